@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s and frames/s of the MI355X render path.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N>1
+launched by torch.distributed.run, one rank per GPU.  One step = one frame
+of the configured workload (default C2 = BASELINE.json configs[1]: 512^3
+procedural world, 1920x1080, primary + 1 sun-shadow ray per pixel), inputs
+resident in HBM.  W untimed frames, then K timed frames bracketed by a
+barrier + device synchronize on both sides; the time is the max over ranks.
+Rank 0 prints ONE JSON line.
+
+Multi-GPU: the frame is split into interleaved 64x64 screen tiles (round
+robin over ranks), every rank renders its tiles of the same frame against
+its own locally generated replica of the world, and rank 0 gathers the
+packed RGBA8 tiles over RCCL (torch.distributed "nccl") and scatters them
+into the frame: strong scaling of a fixed frame.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(st: dict, px: int, halfpx: int, prepass: bool, stage: str) -> int:
+    """4 B per DDA voxel test, 1 B per CSDF read (sphere step or
+    every-8th-step check), 5 B per cone step (1 B CSDF + 4 B GI), 16 B per
+    texture sample; full-res px: 10 B of outputs (+32 B of half-res taps with
+    the pre-pass); half-res px: 8 B of outputs."""
+    b = 4 * st["dda_steps"] + st["sphere_steps"] + st["csdf_checks"]
+    if stage == "render":
+        b += 5 * st["cone_steps"] + 16 * st["tex_samples"] + px * (10 + (32 if prepass else 0))
+    else:
+        b += halfpx * 8
+    return int(b)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", help="c1..c5 (default c2 = BASELINE configs[1])")
+    ap.add_argument("--pose", default="P0")
+    ap.add_argument("--tile-px", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU-baseline budget (rank 0, N=1); 0 disables")
+    ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
+    args = ap.parse_args()
+
+    import torch
+    import rvgrt_amd as rv
+    from rvgrt_amd.atlas import load_atlas, write_png
+    from rvgrt_amd.configs import CONFIGS, pose_f32
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world_size > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local_rank)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    cfg = CONFIGS[args.config]
+    W, H = cfg.width, cfg.height
+    flags = cfg.flags
+    prepass = bool(flags & rv.RV_F_PREPASS)
+    atlas = load_atlas()
+
+    # ---------------------------------------------------------------- world
+    r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=flags, atlas=atlas, device=local_rank)
+    stream = torch.cuda.current_stream(dev)
+    r.set_stream(stream.cuda_stream)
+    t0 = time.perf_counter()
+    r.world_build()
+    for s in range(max(cfg.gi_sweeps, 0)):
+        r.gi_update(s)
+    r.sync()
+    world_s = time.perf_counter() - t0
+    log(f"[rank {rank}] world {cfg.n}^3 built in {world_s:.2f}s")
+
+    pos, yaw, pitch = pose_f32(cfg, args.pose)
+    cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
+
+    # ---------------------------------------------------------------- work census
+    # One full frame with counters on: rays per frame and algorithmic bytes.
+    r.stats_reset()
+    r.frame(cam, vp, flags=flags | rv.RV_F_STATS)
+    st_all = r.stats(-1)
+    st_render = r.stats(0)
+    st_pp = r.stats(1)
+    rays_per_frame = st_all["traces"]
+    b_render = algorithmic_bytes(st_render, W * H, (W // 2) * (H // 2), prepass, "render")
+    b_pp = algorithmic_bytes(st_pp, W * H, (W // 2) * (H // 2), prepass, "prepass") if prepass else 0
+
+    # ---------------------------------------------------------------- tiles
+    T = args.tile_px
+    tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
+    ntiles = tiles_x * tiles_y
+    my_tiles = np.arange(rank, ntiles, world_size, dtype=np.int32)
+    max_per = (ntiles + world_size - 1) // world_size
+    all_ids = [np.arange(q, ntiles, world_size, dtype=np.int32) for q in range(world_size)]
+    if world_size > 1:
+        tbuf = torch.empty(max_per * T * T * 4, dtype=torch.uint8, device=dev)
+        r.bind_tile_buffer(tbuf.data_ptr(), tbuf.numel())
+        gather_list = ([torch.empty_like(tbuf) for _ in range(world_size)] if rank == 0 else None)
+
+    def step():
+        if cfg.gi_per_frame:
+            r.update_gi_data()       # renderLoop: UpdateGIData before drawCUDA
+        if world_size == 1:
+            r.frame(cam, vp, flags=flags)
+        else:
+            r.frame_tiles(cam, vp, my_tiles, tile_px=T, flags=flags)
+            dist.gather(tbuf, gather_list, dst=0)
+            if rank == 0:
+                for q in range(world_size):
+                    r.untile(gather_list[q].data_ptr(), all_ids[q], tile_px=T)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+
+    r.timing_enable(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    stage_ms, nframes = r.timing_get()
+    r.timing_enable(0)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if args.dump and rank == 0:
+        write_png(args.dump, r.readback(rv.RV_IMAGE_COLOR))
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    fps = args.steps / elapsed
+    mrays = rays_per_frame * fps / 1e6
+
+    # dominant kernel: the render stage (k_render / k_render_tiles)
+    render_ms = stage_ms[2] / max(nframes, 1)
+    pp_ms = stage_ms[1] / max(nframes, 1)
+    gi_ms = stage_ms[0] / max(nframes, 1)
+    if world_size == 1:
+        achieved = b_render / (render_ms * 1e-3) / 1e9 if render_ms > 0 else 0.0
+    else:   # per-GPU: this rank's share of the render bytes over its render time
+        achieved = (b_render * len(my_tiles) / ntiles) / (render_ms * 1e-3) / 1e9 if render_ms > 0 else 0.0
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": "k_render", "achieved": round(achieved, 2),
+                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": traffic, "algorithmic_bytes_per_launch": b_render,
+                "avg_launch_ms": round(render_ms, 4)}
+
+    # ---------------------------------------------------------------- CPU baseline
+    cpu = None
+    if rank == 0 and world_size == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(r, cfg, cam, vp, flags, atlas, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": f"Mrays/s ({cfg.name}: {cfg.describe})",
+            "value": round(mrays, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "fps": round(fps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: procedural world from the reference Evaluate (seed 0), camera pose "
+                    f"{args.pose} (reference defaults), random-free",
+            "config": {"workload": cfg.name, "world": f"{cfg.n}^3", "resolution": f"{W}x{H}",
+                       "flags": flags, "gi_sweeps": cfg.gi_sweeps, "gi_update_per_frame": cfg.gi_per_frame,
+                       "parallelism": f"screen-tiles {T}px x{world_size}" if world_size > 1 else "single-gpu"},
+            "rays_per_frame": rays_per_frame,
+            "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "world_build_s": round(world_s, 3),
+            "stats": st_all,
+        }
+        print(json.dumps(line), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
+    """The CPU oracle (scalar DDA restatement) on the host cores, same world
+    (exported from the GPU; bit-identical to the oracle's own build, see
+    tests/test_gpu_parity.py), same camera and features.  Bounded sample:
+    whole frames until the budget is spent, else a stride-k row subset."""
+    import rvgrt_amd as rv
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    w = O.OracleWorld(cfg.log2_n, cfg.log2_n, cfg.log2_n, atlas=atlas)
+    w.bits[:] = r.world_export(rv.RV_WORLD_BITS)
+    w.csdf[:] = r.world_export(rv.RV_WORLD_CSDF)
+    w.gi[:] = r.world_export(rv.RV_WORLD_GI)
+    fr = O.make_frame(cfg.width, cfg.height, flags, rv.camera_dict(cam, vp))
+    # bands of rows spread over the image (OpenMP parallel over a band's rows)
+    H = cfg.height
+    band = max(8, 2 * threads)
+    starts = list(range(0, H, band))
+    order = [s for k in range(4) for s in starts[k::4]]
+    t0 = time.perf_counter()
+    rays = rows = 0
+    for s in order:
+        out = O.render(w, fr, s, min(H, s + band))
+        rays += out["stats"]["traces"]
+        rows += min(H, s + band) - s
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/rv_oracle.c render of {rows}/{H} rows of {cfg.name} in {band}-row bands "
+                      f"({dt:.1f}s, {rays} traces), same world/camera/flags"}
+
+
+if __name__ == "__main__":
+    main()

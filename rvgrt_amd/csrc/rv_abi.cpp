@@ -1,0 +1,656 @@
+// rv_abi.cpp -- host side of librvgrt_hip.so: the C ABI declared in
+// include/rvgrt.h.  Owns device memory, the HIP stream and the GI update
+// state; every entry point converts failures into rv_status + message.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rv_internal.h"
+
+using namespace rv;
+
+struct rv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    rv_config cfg{};
+    int lx = 0, ly = 0, lz = 0;
+    World w{};
+    uint32_t* brick = nullptr;
+    size_t brick_bytes = 0;
+    uint32_t* gi = nullptr;       // current grid
+    uint32_t* gi_tmp = nullptr;   // update target (double buffer)
+    size_t gi_bytes = 0;
+    uint32_t* atlas = nullptr;
+    // frame images (library-owned unless bound)
+    uint32_t* color = nullptr; size_t color_pitch = 0; bool color_ext = false;
+    uint32_t* mv = nullptr; size_t mv_pitch = 0; bool mv_ext = false;
+    uint16_t* depth = nullptr; size_t depth_pitch = 0; bool depth_ext = false;
+    uint32_t* own_color = nullptr; uint32_t* own_mv = nullptr; uint16_t* own_depth = nullptr;
+    size_t own_color_pitch = 0, own_mv_pitch = 0, own_depth_pitch = 0;
+    float* hdist = nullptr;
+    float* hshadow = nullptr;
+    unsigned long long* counters = nullptr;
+    int* tile_ids = nullptr; int tile_cap = 0;
+    uint32_t* tilebuf = nullptr; size_t tilebuf_bytes = 0;
+    uint32_t* ext_tilebuf = nullptr; size_t ext_tilebuf_bytes = 0;
+    // stage timing (rv_timing_enable): 4 events per frame
+    int timing_cap = 0, timing_n = 0;
+    bool gi_pending = false;
+    std::vector<hipEvent_t> ev;
+    uint32_t gi_frame = 0;
+    uint64_t gi_offset = 0;
+    bool world_ready = false;
+    std::string err;
+};
+
+namespace {
+
+rv_status fail(rv_ctx* c, rv_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? RV_ERR_OOM : RV_ERR_HIP,          \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+    } while (0)
+
+#define LAUNCH_CHECK(ctx) HIP_TRY(ctx, hipGetLastError())
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+uint64_t n_gi(const rv_ctx* c) { return (uint64_t)c->w.GX * c->w.GY * c->w.GZ; }
+uint64_t n_csdf(const rv_ctx* c) { return (uint64_t)c->w.SX * c->w.SY * c->w.SZ; }
+uint64_t n_bits_words(const rv_ctx* c) { return ((uint64_t)c->w.X * c->w.Y * c->w.Z) >> 5; }
+
+f3 host_v(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+
+// glm::normalize(vec3(10,5,-4)) (src/StateRender.cu:299, src/CoarseArray.cu:359)
+f3 sun_dir() {
+    float d = 10.0f * 10.0f + 5.0f * 5.0f + (-4.0f) * (-4.0f);
+    float inv = 1.0f / sqrtf(d);
+    return host_v(10.0f * inv, 5.0f * inv, -4.0f * inv);
+}
+
+World current_world(const rv_ctx* c) {
+    World w = c->w;
+    w.brick = c->brick;
+    w.gi = c->gi;
+    w.atlas = c->atlas;
+    return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rv_abi_version(void) { return RVGRT_ABI_VERSION; }
+
+const char* rv_last_error(const rv_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
+    if (!cfg || !out) return RV_ERR_INVALID;
+    *out = nullptr;
+    if (cfg->log2_x < 4 || cfg->log2_y < 4 || cfg->log2_z < 4 || cfg->log2_x > 13 || cfg->log2_y > 13 ||
+        cfg->log2_z > 13)
+        return RV_ERR_INVALID;
+    if (cfg->width < 2 || cfg->height < 2 || (cfg->width & 1) || (cfg->height & 1)) return RV_ERR_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return RV_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RV_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RV_ERR_NO_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return RV_ERR_NO_DEVICE;
+
+    rv_ctx* c = new rv_ctx();
+    c->device = device;
+    c->cfg = *cfg;
+    if (c->cfg.gi_rays_per_frame == 0) c->cfg.gi_rays_per_frame = 64 * 64 * 64;
+    c->lx = cfg->log2_x; c->ly = cfg->log2_y; c->lz = cfg->log2_z;
+    World& w = c->w;
+    w.X = 1 << c->lx; w.Y = 1 << c->ly; w.Z = 1 << c->lz;
+    w.lbx = c->lx - 3; w.lbxy = (c->lx - 3) + (c->ly - 3);
+    w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
+    w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
+    w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
+    c->brick_bytes = ((uint64_t)w.X * w.Y * w.Z) / 4;   // 128 B per 512 voxels
+    c->gi_bytes = n_gi(c) * 4;
+
+    auto cleanup_fail = [&](rv_status s, const char* what) {
+        std::string m = std::string("rv_create: ") + what;
+        rv_destroy(c);
+        (void)m;
+        return s;
+    };
+    if (hipMalloc(&c->brick, c->brick_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "bricks");
+    if (hipMalloc(&c->gi, c->gi_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "gi");
+    hipMemset(c->brick, 0, c->brick_bytes);
+    hipMemset(c->gi, 0, c->gi_bytes);
+    // atlas
+    int aw = cfg->atlas_rgba8 ? cfg->atlas_w : 256, ah = cfg->atlas_rgba8 ? cfg->atlas_h : 256;
+    if (aw <= 0 || ah <= 0) return cleanup_fail(RV_ERR_INVALID, "atlas dims");
+    w.aw = aw; w.ah = ah;
+    if (hipMalloc(&c->atlas, (size_t)aw * ah * 4) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "atlas");
+    if (cfg->atlas_rgba8) {
+        hipMemcpy(c->atlas, cfg->atlas_rgba8, (size_t)aw * ah * 4, hipMemcpyHostToDevice);
+    } else {
+        std::vector<uint32_t> grey((size_t)aw * ah, 0xFF808080u);
+        hipMemcpy(c->atlas, grey.data(), grey.size() * 4, hipMemcpyHostToDevice);
+    }
+    c->cfg.atlas_rgba8 = nullptr;
+    // frame images, rows padded to 256 B like a D3D12 placed footprint
+    int W = cfg->width, H = cfg->height;
+    c->own_color_pitch = align256((size_t)W * 4);
+    c->own_mv_pitch = align256((size_t)W * 4);
+    c->own_depth_pitch = align256((size_t)W * 2);
+    if (hipMalloc(&c->own_color, c->own_color_pitch * H) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "color");
+    if (hipMalloc(&c->own_mv, c->own_mv_pitch * H) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "mv");
+    if (hipMalloc(&c->own_depth, c->own_depth_pitch * H) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "depth");
+    hipMemset(c->own_color, 0, c->own_color_pitch * H);
+    hipMemset(c->own_mv, 0, c->own_mv_pitch * H);
+    hipMemset(c->own_depth, 0, c->own_depth_pitch * H);
+    c->color = c->own_color; c->color_pitch = c->own_color_pitch;
+    c->mv = c->own_mv; c->mv_pitch = c->own_mv_pitch;
+    c->depth = c->own_depth; c->depth_pitch = c->own_depth_pitch;
+    size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    if (hipMalloc(&c->hdist, hbytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "halfdist");
+    if (hipMalloc(&c->hshadow, hbytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "halfshadow");
+    hipMemset(c->hdist, 0, hbytes);
+    hipMemset(c->hshadow, 0, hbytes);
+    if (hipMalloc(&c->counters, 2 * NCNT * sizeof(unsigned long long)) != hipSuccess)
+        return cleanup_fail(RV_ERR_OOM, "counters");
+    hipMemset(c->counters, 0, 2 * NCNT * sizeof(unsigned long long));
+    if (hipDeviceSynchronize() != hipSuccess) return cleanup_fail(RV_ERR_HIP, "init sync");
+    *out = c;
+    return RV_OK;
+}
+
+void rv_destroy(rv_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream); else hipDeviceSynchronize();
+    hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
+    hipFree(c->own_color); hipFree(c->own_mv); hipFree(c->own_depth);
+    hipFree(c->hdist); hipFree(c->hshadow); hipFree(c->counters);
+    hipFree(c->tile_ids); hipFree(c->tilebuf);
+    for (hipEvent_t e : c->ev) hipEventDestroy(e);
+    delete c;
+}
+
+rv_status rv_set_stream(rv_ctx* c, void* s) {
+    if (!c) return RV_ERR_INVALID;
+    c->stream = (hipStream_t)s;
+    return RV_OK;
+}
+
+rv_status rv_sync(rv_ctx* c) {
+    if (!c) return RV_ERR_INVALID;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RV_OK;
+}
+
+rv_status rv_csdf_build(rv_ctx* c) {
+    if (!c) return RV_ERR_INVALID;
+    uint64_t n = n_csdf(c);
+    uint8_t *t0 = nullptr, *t1 = nullptr;
+    HIP_TRY(c, hipMallocAsync((void**)&t0, n, c->stream));
+    HIP_TRY(c, hipMallocAsync((void**)&t1, n, c->stream));
+    launch_csdf(c->stream, c->brick, current_world(c), t0, t1);
+    LAUNCH_CHECK(c);
+    HIP_TRY(c, hipFreeAsync(t0, c->stream));
+    HIP_TRY(c, hipFreeAsync(t1, c->stream));
+    return RV_OK;
+}
+
+rv_status rv_gi_init(rv_ctx* c) {
+    if (!c) return RV_ERR_INVALID;
+    launch_gi_init(c->stream, c->gi, current_world(c), sun_dir(), c->counters);
+    LAUNCH_CHECK(c);
+    c->gi_frame = 0;
+    c->gi_offset = 0;
+    return RV_OK;
+}
+
+rv_status rv_world_build(rv_ctx* c) {
+    if (!c) return RV_ERR_INVALID;
+    launch_fill_bricks(c->stream, c->brick, current_world(c), c->cfg.seed_x, c->cfg.seed_z);
+    LAUNCH_CHECK(c);
+    rv_status s = rv_csdf_build(c);
+    if (s != RV_OK) return s;
+    s = rv_gi_init(c);
+    if (s != RV_OK) return s;
+    c->world_ready = true;
+    return RV_OK;
+}
+
+rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t bytes) {
+    if (!c || !host) return RV_ERR_INVALID;
+    if (kind == RV_WORLD_BITS) {
+        if (bytes != n_bits_words(c) * 4) return fail(c, RV_ERR_INVALID, "bits size mismatch");
+        uint32_t* d = nullptr;
+        HIP_TRY(c, hipMalloc(&d, bytes));
+        HIP_TRY(c, hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, c->stream));
+        launch_bits_import(c->stream, d, c->brick, current_world(c), c->lx, c->ly);
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        hipFree(d);
+    } else if (kind == RV_WORLD_CSDF) {
+        if (bytes != n_csdf(c)) return fail(c, RV_ERR_INVALID, "csdf size mismatch");
+        uint8_t* d = nullptr;
+        HIP_TRY(c, hipMalloc(&d, bytes));
+        HIP_TRY(c, hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, c->stream));
+        launch_csdf_import(c->stream, d, c->brick, current_world(c));
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        hipFree(d);
+    } else if (kind == RV_WORLD_GI) {
+        if (bytes != c->gi_bytes) return fail(c, RV_ERR_INVALID, "gi size mismatch");
+        HIP_TRY(c, hipMemcpyAsync(c->gi, host, bytes, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else {
+        return fail(c, RV_ERR_INVALID, "bad world kind");
+    }
+    c->world_ready = true;
+    return RV_OK;
+}
+
+rv_status rv_world_export(rv_ctx* c, int32_t kind, void* host, size_t bytes) {
+    if (!c || !host) return RV_ERR_INVALID;
+    if (kind == RV_WORLD_BITS) {
+        if (bytes != n_bits_words(c) * 4) return fail(c, RV_ERR_INVALID, "bits size mismatch");
+        uint32_t* d = nullptr;
+        HIP_TRY(c, hipMalloc(&d, bytes));
+        launch_bits_export(c->stream, c->brick, d, current_world(c), c->lx, c->ly);
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, hipMemcpyAsync(host, d, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        hipFree(d);
+    } else if (kind == RV_WORLD_CSDF) {
+        if (bytes != n_csdf(c)) return fail(c, RV_ERR_INVALID, "csdf size mismatch");
+        uint8_t* d = nullptr;
+        HIP_TRY(c, hipMalloc(&d, bytes));
+        launch_csdf_export(c->stream, c->brick, d, current_world(c));
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, hipMemcpyAsync(host, d, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        hipFree(d);
+    } else if (kind == RV_WORLD_GI) {
+        if (bytes != c->gi_bytes) return fail(c, RV_ERR_INVALID, "gi size mismatch");
+        HIP_TRY(c, hipMemcpyAsync(host, c->gi, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else {
+        return fail(c, RV_ERR_INVALID, "bad world kind");
+    }
+    return RV_OK;
+}
+
+rv_status rv_gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t count) {
+    if (!c) return RV_ERR_INVALID;
+    uint64_t n = n_gi(c);
+    if (first >= n) return RV_OK;
+    if (first + count > n) count = n - first;
+    if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
+    launch_gi_update(c->stream, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count, c->counters);
+    LAUNCH_CHECK(c);
+    if (count == n) {
+        std::swap(c->gi, c->gi_tmp);   // full sweep: flip the double buffer
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice,
+                                  c->stream));
+    }
+    return RV_OK;
+}
+
+rv_status rv_update_gi_data(rv_ctx* c) {
+    if (!c) return RV_ERR_INVALID;
+    uint64_t rays = c->cfg.gi_rays_per_frame, n = n_gi(c);
+    if (c->timing_n < c->timing_cap) {
+        HIP_TRY(c, hipEventRecord(c->ev[4 * c->timing_n + 0], c->stream));
+        c->gi_pending = true;
+    }
+    rv_status s = rv_gi_update(c, c->gi_frame, c->gi_offset, rays);
+    if (s != RV_OK) return s;
+    c->gi_frame++;
+    if (c->gi_offset + rays >= n) c->gi_offset = 0;   // src/CoarseArray.cu:392-394
+    else c->gi_offset += rays;
+    return RV_OK;
+}
+
+static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp, const float* pvp, float time,
+                               float jx, float jy, int32_t flags) {
+    FrameParams f{};
+    f.pos = host_v(cam->pos[0], cam->pos[1], cam->pos[2]);
+    f.fo = host_v(cam->forward[0], cam->forward[1], cam->forward[2]);
+    f.ri = host_v(cam->right[0], cam->right[1], cam->right[2]);
+    f.up = host_v(cam->up[0], cam->up[1], cam->up[2]);
+    f.sun = sun_dir();
+    f.time = time; f.jx = jx; f.jy = jy;
+    for (int i = 0; i < 16; i++) {
+        f.vp[i] = vp ? vp[i] : (i % 5 == 0 ? 1.0f : 0.0f);
+        f.pvp[i] = pvp ? pvp[i] : f.vp[i];
+    }
+    f.W = c->cfg.width; f.H = c->cfg.height; f.hw = f.W / 2; f.hh = f.H / 2;
+    f.flags = flags;
+    f.color = c->color; f.color_pitch = c->color_pitch;
+    f.mv = c->mv; f.mv_pitch = c->mv_pitch;
+    f.depth = c->depth; f.depth_pitch = c->depth_pitch;
+    f.hdist = c->hdist; f.hshadow = c->hshadow;
+    f.counters = c->counters;
+    return f;
+}
+
+// Enqueue pre-pass + render, recording stage events when timing is on.
+static rv_status run_stages(rv_ctx* c, const FrameParams& f, bool tiles) {
+    bool timed = c->timing_n < c->timing_cap;
+    hipEvent_t* e = timed ? &c->ev[4 * c->timing_n] : nullptr;
+    World w = current_world(c);
+    if (timed) {
+        if (!c->gi_pending) HIP_TRY(c, hipEventRecord(e[0], c->stream));
+        HIP_TRY(c, hipEventRecord(e[1], c->stream));
+    }
+    if (f.flags & RV_F_PREPASS) {
+        FrameParams fp = f;
+        fp.counters = c->counters + NCNT;   // pre-pass counters kept apart (rv_stats_stage)
+        if (tiles) launch_prepass_tiles(c->stream, w, fp); else launch_prepass(c->stream, w, fp);
+        LAUNCH_CHECK(c);
+    }
+    if (timed) HIP_TRY(c, hipEventRecord(e[2], c->stream));
+    if (tiles) launch_render_tiles(c->stream, w, f); else launch_render(c->stream, w, f);
+    LAUNCH_CHECK(c);
+    if (timed) {
+        HIP_TRY(c, hipEventRecord(e[3], c->stream));
+        c->timing_n++;
+        c->gi_pending = false;
+    }
+    return RV_OK;
+}
+
+rv_status rv_frame(rv_ctx* c, const rv_camera* cam, const float* vp16, const float* pvp16, float time,
+                   float jx, float jy, int32_t flags) {
+    if (!c || !cam) return RV_ERR_INVALID;
+    if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_frame before rv_world_build/import");
+    FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+    return run_stages(c, f, false);
+}
+
+rv_status rv_draw_cuda(rv_ctx* c, const float pos[3], const float fo[3], const float up[3], const float ri[3],
+                       const float* vp16, const float* pvp16, float jitter_x, float jitter_y) {
+    if (!c || !pos || !fo || !up || !ri) return RV_ERR_INVALID;
+    rv_camera cam{};
+    for (int i = 0; i < 3; i++) { cam.pos[i] = pos[i]; cam.forward[i] = fo[i]; cam.up[i] = up[i]; cam.right[i] = ri[i]; }
+    float time, jx, jy;
+    if (c->cfg.ref_compat) {
+        // c_time = c_cam[17] = host jitterY; c_jitterX = c_cam[18] (never
+        // written, 0); c_jitterY = c_cam[19] (4 B past the symbol).
+        time = jitter_y; jx = 0.0f; jy = c->cfg.ref_oob_jy;
+    } else {
+        long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                           std::chrono::system_clock::now().time_since_epoch()).count();
+        time = (float)(ms % 1000000) * 0.001f;
+        jx = jitter_x; jy = jitter_y;
+    }
+    return rv_frame(c, &cam, vp16, pvp16, time, jx, jy, c->cfg.flags);
+}
+
+rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, const float* pvp16, float time,
+                         float jx, float jy, int32_t flags, const int32_t* tile_ids, int32_t ntiles,
+                         int32_t tile_px) {
+    if (!c || !cam || (ntiles > 0 && !tile_ids) || ntiles < 0) return RV_ERR_INVALID;
+    if (tile_px < 16 || (tile_px & 15)) return fail(c, RV_ERR_INVALID, "tile_px must be a multiple of 16");
+    if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_frame_tiles before world");
+    int tiles_x = (c->cfg.width + tile_px - 1) / tile_px;
+    int tiles_y = (c->cfg.height + tile_px - 1) / tile_px;
+    for (int i = 0; i < ntiles; i++)
+        if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(c, RV_ERR_INVALID, "tile id out of range");
+    if (ntiles > c->tile_cap) {
+        hipFree(c->tile_ids);
+        c->tile_ids = nullptr;
+        HIP_TRY(c, hipMalloc(&c->tile_ids, (size_t)ntiles * 4));
+        c->tile_cap = ntiles;
+    }
+    size_t need = (size_t)ntiles * tile_px * tile_px * 4;
+    if (!c->ext_tilebuf && need > c->tilebuf_bytes) {
+        hipFree(c->tilebuf);
+        c->tilebuf = nullptr;
+        HIP_TRY(c, hipMalloc(&c->tilebuf, need));
+        c->tilebuf_bytes = need;
+    }
+    if (ntiles > 0)
+        HIP_TRY(c, hipMemcpyAsync(c->tile_ids, tile_ids, (size_t)ntiles * 4, hipMemcpyHostToDevice, c->stream));
+    FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+    f.tiles = c->tile_ids; f.ntiles = ntiles; f.tile_px = tile_px; f.tiles_x = tiles_x;
+    f.tilebuf = c->ext_tilebuf ? c->ext_tilebuf : c->tilebuf;
+    if (c->ext_tilebuf && need > c->ext_tilebuf_bytes) return fail(c, RV_ERR_INVALID, "bound tile buffer too small");
+    return run_stages(c, f, true);
+}
+
+rv_status rv_tile_buffer(rv_ctx* c, void** p, size_t* bytes) {
+    if (!c || !p) return RV_ERR_INVALID;
+    *p = c->ext_tilebuf ? c->ext_tilebuf : c->tilebuf;
+    if (bytes) *bytes = c->ext_tilebuf ? c->ext_tilebuf_bytes : c->tilebuf_bytes;
+    return RV_OK;
+}
+
+rv_status rv_bind_tile_buffer(rv_ctx* c, void* p, size_t bytes) {
+    if (!c) return RV_ERR_INVALID;
+    c->ext_tilebuf = (uint32_t*)p;
+    c->ext_tilebuf_bytes = p ? bytes : 0;
+    return RV_OK;
+}
+
+rv_status rv_timing_enable(rv_ctx* c, int32_t max_frames) {
+    if (!c || max_frames < 0) return RV_ERR_INVALID;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (hipEvent_t e : c->ev) hipEventDestroy(e);
+    c->ev.clear();
+    c->timing_cap = 0; c->timing_n = 0; c->gi_pending = false;
+    c->ev.resize((size_t)max_frames * 4);
+    for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
+    c->timing_cap = max_frames;
+    return RV_OK;
+}
+
+rv_status rv_timing_get(rv_ctx* c, double ms[3], int32_t* frames) {
+    if (!c || !ms) return RV_ERR_INVALID;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    ms[0] = ms[1] = ms[2] = 0.0;
+    for (int i = 0; i < c->timing_n; i++) {
+        for (int k = 0; k < 3; k++) {
+            float t = 0.0f;
+            HIP_TRY(c, hipEventElapsedTime(&t, c->ev[4 * i + k], c->ev[4 * i + k + 1]));
+            ms[k] += t;
+        }
+    }
+    if (frames) *frames = c->timing_n;
+    return RV_OK;
+}
+
+rv_status rv_untile(rv_ctx* c, const void* dev_tiles, const int32_t* tile_ids, int32_t ntiles, int32_t tile_px) {
+    if (!c || (ntiles > 0 && (!dev_tiles || !tile_ids)) || tile_px <= 0) return RV_ERR_INVALID;
+    int tiles_x = (c->cfg.width + tile_px - 1) / tile_px;
+    int tiles_y = (c->cfg.height + tile_px - 1) / tile_px;
+    for (int i = 0; i < ntiles; i++)
+        if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(c, RV_ERR_INVALID, "tile id out of range");
+    int* ids = nullptr;
+    HIP_TRY(c, hipMallocAsync((void**)&ids, (size_t)(ntiles > 0 ? ntiles : 1) * 4, c->stream));
+    if (ntiles > 0)
+        HIP_TRY(c, hipMemcpyAsync(ids, tile_ids, (size_t)ntiles * 4, hipMemcpyHostToDevice, c->stream));
+    launch_untile(c->stream, (const uint32_t*)dev_tiles, ids, ntiles, tile_px, tiles_x, c->cfg.width,
+                  c->cfg.height, c->color, c->color_pitch);
+    LAUNCH_CHECK(c);
+    HIP_TRY(c, hipFreeAsync(ids, c->stream));
+    return RV_OK;
+}
+
+rv_status rv_bind_output(rv_ctx* c, int32_t kind, void* p, size_t pitch) {
+    if (!c) return RV_ERR_INVALID;
+    size_t W = (size_t)c->cfg.width;
+    switch (kind) {
+    case RV_IMAGE_COLOR:
+        if (p && pitch < W * 4) return fail(c, RV_ERR_INVALID, "pitch too small");
+        c->color = p ? (uint32_t*)p : c->own_color;
+        c->color_pitch = p ? pitch : c->own_color_pitch;
+        c->color_ext = p != nullptr;
+        return RV_OK;
+    case RV_IMAGE_MOTION:
+        if (p && pitch < W * 4) return fail(c, RV_ERR_INVALID, "pitch too small");
+        c->mv = p ? (uint32_t*)p : c->own_mv;
+        c->mv_pitch = p ? pitch : c->own_mv_pitch;
+        c->mv_ext = p != nullptr;
+        return RV_OK;
+    case RV_IMAGE_DEPTH:
+        if (p && pitch < W * 2) return fail(c, RV_ERR_INVALID, "pitch too small");
+        c->depth = p ? (uint16_t*)p : c->own_depth;
+        c->depth_pitch = p ? pitch : c->own_depth_pitch;
+        c->depth_ext = p != nullptr;
+        return RV_OK;
+    default:
+        return fail(c, RV_ERR_INVALID, "bad image kind");
+    }
+}
+
+static rv_status image_desc(rv_ctx* c, int32_t kind, void** p, size_t* pitch, size_t* row_bytes, int* rows) {
+    int W = c->cfg.width, H = c->cfg.height;
+    switch (kind) {
+    case RV_IMAGE_COLOR: *p = c->color; *pitch = c->color_pitch; *row_bytes = (size_t)W * 4; *rows = H; return RV_OK;
+    case RV_IMAGE_MOTION: *p = c->mv; *pitch = c->mv_pitch; *row_bytes = (size_t)W * 4; *rows = H; return RV_OK;
+    case RV_IMAGE_DEPTH: *p = c->depth; *pitch = c->depth_pitch; *row_bytes = (size_t)W * 2; *rows = H; return RV_OK;
+    case RV_IMAGE_HALF_DIST:
+        *p = c->hdist; *pitch = (size_t)(W / 2) * 4; *row_bytes = *pitch; *rows = H / 2; return RV_OK;
+    case RV_IMAGE_HALF_SHADOW:
+        *p = c->hshadow; *pitch = (size_t)(W / 2) * 4; *row_bytes = *pitch; *rows = H / 2; return RV_OK;
+    default: return fail(c, RV_ERR_INVALID, "bad image kind");
+    }
+}
+
+rv_status rv_image_ptr(rv_ctx* c, int32_t kind, void** p, size_t* pitch) {
+    if (!c || !p) return RV_ERR_INVALID;
+    size_t pt, rb; int rows;
+    rv_status s = image_desc(c, kind, p, &pt, &rb, &rows);
+    if (pitch) *pitch = pt;
+    return s;
+}
+
+rv_status rv_readback(rv_ctx* c, int32_t kind, void* host, size_t pitch) {
+    if (!c || !host) return RV_ERR_INVALID;
+    void* p; size_t dp, rb; int rows;
+    rv_status s = image_desc(c, kind, &p, &dp, &rb, &rows);
+    if (s != RV_OK) return s;
+    if (pitch == 0) pitch = rb;
+    if (pitch < rb) return fail(c, RV_ERR_INVALID, "host pitch too small");
+    HIP_TRY(c, hipMemcpy2DAsync(host, pitch, p, dp, rb, rows, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RV_OK;
+}
+
+rv_status rv_trace_rays(rv_ctx* c, const float* org, const float* dir, const float* dist, int64_t n, rv_hit* out) {
+    if (!c || n < 0 || (n > 0 && (!org || !dir || !dist || !out))) return RV_ERR_INVALID;
+    if (n == 0) return RV_OK;
+    float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr;
+    RvHitDev* d_h = nullptr;
+    HIP_TRY(c, hipMalloc(&d_o, (size_t)n * 12));
+    HIP_TRY(c, hipMalloc(&d_d, (size_t)n * 12));
+    HIP_TRY(c, hipMalloc(&d_t, (size_t)n * 4));
+    HIP_TRY(c, hipMalloc(&d_h, (size_t)n * sizeof(RvHitDev)));
+    HIP_TRY(c, hipMemcpyAsync(d_o, org, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(d_d, dir, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(d_t, dist, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    launch_trace_rays(c->stream, current_world(c), d_o, d_d, d_t, n, d_h);
+    LAUNCH_CHECK(c);
+    HIP_TRY(c, hipMemcpyAsync(out, d_h, (size_t)n * sizeof(RvHitDev), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    hipFree(d_o); hipFree(d_d); hipFree(d_t); hipFree(d_h);
+    return RV_OK;
+}
+
+// Character::Update camera math (src/Character.cpp:18-126) for a static pose.
+static f3 glm_norm(f3 v) {
+    float d = v.x * v.x + v.y * v.y + v.z * v.z;
+    float inv = 1.0f / sqrtf(d);
+    return host_v(v.x * inv, v.y * inv, v.z * inv);
+}
+static f3 h_cross(f3 a, f3 b) {
+    return host_v(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+rv_status rv_camera_from_pose(float px, float py, float pz, float yaw, float pitch, int32_t width, int32_t height,
+                              rv_camera* cam, float* vp16) {
+    if (!cam || width <= 0 || height <= 0) return RV_ERR_INVALID;
+    const float pih = 3.14159265358979323846f * 0.5f;
+    float s0 = sinf((float)(double)yaw), s1 = sinf((float)((double)yaw + (double)pih));
+    float s2 = sinf((float)(double)pitch), s3 = sinf((float)((double)pitch + (double)pih));
+    f3 dir = glm_norm(host_v(-s0 * -s3, -s2, -s1 * s3));
+    f3 right = glm_norm(h_cross(dir, host_v(0.0f, 1.0f, 0.0f)));
+    f3 up = glm_norm(h_cross(dir, right));
+    std::memset(cam, 0, sizeof(*cam));
+    cam->pos[0] = px; cam->pos[1] = py; cam->pos[2] = pz;
+    cam->forward[0] = dir.x; cam->forward[1] = dir.y; cam->forward[2] = dir.z;
+    cam->right[0] = right.x; cam->right[1] = right.y; cam->right[2] = right.z;
+    cam->up[0] = up.x; cam->up[1] = up.y; cam->up[2] = up.z;
+    float fov_factor = (float)tan(60.0f * 3.14159265358979323846 / 180.0);
+    float aspect = (float)width / (float)height;
+    cam->add[0] = aspect * -fov_factor; cam->add[1] = 1.0f * -fov_factor;
+    cam->mul[0] = fov_factor * aspect * (2.0f / (float)width);
+    cam->mul[1] = fov_factor * 1.0f * (2.0f / (float)height);
+    if (vp16) {
+        f3 eye = host_v(px, py, pz);
+        f3 ctr = host_v(eye.x + dir.x, eye.y + dir.y, eye.z + dir.z);
+        f3 f = glm_norm(host_v(ctr.x - eye.x, ctr.y - eye.y, ctr.z - eye.z));
+        f3 s = glm_norm(h_cross(f, host_v(0.0f, 1.0f, 0.0f)));
+        f3 u = h_cross(s, f);
+        float view[16] = {0};
+        view[0] = s.x; view[4] = s.y; view[8] = s.z;
+        view[1] = u.x; view[5] = u.y; view[9] = u.z;
+        view[2] = -f.x; view[6] = -f.y; view[10] = -f.z;
+        view[12] = -(s.x * eye.x + s.y * eye.y + s.z * eye.z);
+        view[13] = -(u.x * eye.x + u.y * eye.y + u.z * eye.z);
+        view[14] = f.x * eye.x + f.y * eye.y + f.z * eye.z;
+        view[15] = 1.0f;
+        float fovy = 60.0f * 0.01745329251994329576923690768489f;
+        float zn = 0.1f, zf = 50000.0f;
+        float th = tanf(fovy / 2.0f);
+        float proj[16] = {0};
+        proj[0] = 1.0f / (aspect * th);
+        proj[5] = 1.0f / th;
+        proj[10] = -(zf + zn) / (zf - zn);
+        proj[11] = -1.0f;
+        proj[14] = -(2.0f * zf * zn) / (zf - zn);
+        for (int col = 0; col < 4; col++)
+            for (int r = 0; r < 4; r++)
+                vp16[col * 4 + r] = proj[0 * 4 + r] * view[col * 4 + 0] + proj[1 * 4 + r] * view[col * 4 + 1] +
+                                    proj[2 * 4 + r] * view[col * 4 + 2] + proj[3 * 4 + r] * view[col * 4 + 3];
+    }
+    return RV_OK;
+}
+
+// counters: block 0 = everything but the pre-pass, block 1 = pre-pass
+rv_status rv_stats_stage(rv_ctx* c, int32_t stage, rv_stats* out) {
+    if (!c || !out || stage < -1 || stage > 1) return RV_ERR_INVALID;
+    unsigned long long h[2 * NCNT];
+    HIP_TRY(c, hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    static_assert(sizeof(rv_stats) == NCNT * 8, "rv_stats layout");
+    unsigned long long r[NCNT];
+    for (int k = 0; k < NCNT; k++)
+        r[k] = stage < 0 ? h[k] + h[NCNT + k] : h[stage * NCNT + k];
+    std::memcpy(out, r, sizeof(r));
+    return RV_OK;
+}
+
+rv_status rv_stats_get(rv_ctx* c, rv_stats* out) { return rv_stats_stage(c, -1, out); }
+
+rv_status rv_stats_reset(rv_ctx* c) {
+    if (!c) return RV_ERR_INVALID;
+    HIP_TRY(c, hipMemsetAsync(c->counters, 0, 2 * NCNT * sizeof(unsigned long long), c->stream));
+    return RV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,404 @@
+// rv_device.h -- device-side traversal / shading library for gfx950 (CDNA4).
+//
+// MI355X-native restatement of the reference's __device__ API
+// (include/raytracing_functions.cuh:23-84, src/raytracing_functions.cu,
+// include/TerrainGeneration.cuh).  Differences from the reference are in
+// HOW, not WHAT:
+//   * world dims are runtime (power-of-two per axis), indices 64-bit safe;
+//   * voxel bits and the coarse SDF live in one 128-B "brick record" per
+//     8x8x8 voxels (64 B of bits + 64 B of CSDF for the same region), so a
+//     DDA step's bit test and its every-8th-step CSDF check hit one line;
+//   * texture atlas is a plain RGBA8 array sampled with exact point/wrap
+//     semantics instead of a CUDA texture object.
+// Every float operation keeps the reference's order and is separately
+// rounded (the library is built with -ffp-contract=off) so results are
+// bit-identical with the CPU oracle (oracle/rv_oracle.c).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rv {
+
+// ---------------------------------------------------------------- vectors
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 V(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mul(f3 a, f3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 scale(f3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 divs(f3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ f3 neg(f3 a) { return V(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ f3 normalize(f3 v) { float l = length(v); return scale(v, 1.0f / l); }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ f3 lerp(f3 a, f3 b, float t) { return add(a, scale(sub(b, a), t)); }
+__device__ __forceinline__ f3 reflect(f3 I, f3 N) { return sub(I, scale(N, 2.0f * dot(I, N))); }
+__device__ __forceinline__ float clampf(float v, float a, float b) { return fmaxf(a, fminf(b, v)); }
+
+// (float)(half)x with round-to-nearest-even (cuda_fp16 __float2half_rn).
+__device__ __forceinline__ float hround(float x) { return (float)(_Float16)x; }
+__device__ __forceinline__ uint16_t hbits(float x) {
+    _Float16 h = (_Float16)x; return __builtin_bit_cast(uint16_t, h);
+}
+
+// ---------------------------------------------------------------- world view
+// Passed by value as a kernel argument (lands in SGPRs via the kernarg segment).
+struct World {
+    const uint32_t* __restrict__ brick;  // 32 dwords / brick: [0,16) bits, [16,32) CSDF bytes
+    const uint32_t* __restrict__ gi;     // RGBA8 per 4^3 cell, x fastest
+    const uint32_t* __restrict__ atlas;  // RGBA8 atlas, row-major
+    int X, Y, Z;                         // voxel dims
+    int lbx, lbxy;                       // brick id = bx | by<<lbx | bz<<lbxy
+    int SX, SY, SZ;                      // CSDF dims (X/2 ...)
+    int GX, GY, GZ;                      // GI dims (X/4 ...)
+    float fX, fY, fZ;
+    int aw, ah;
+};
+
+__device__ __forceinline__ uint64_t brick_of(const World& w, int bx, int by, int bz) {
+    return (uint64_t)(uint32_t)bx | ((uint64_t)(uint32_t)by << w.lbx) | ((uint64_t)(uint32_t)bz << w.lbxy);
+}
+
+// IsSolid (include/raytracing_functions.cuh:23-26) on the brick layout.
+// Callers pass in-range coordinates (the reference bounds-checks first).
+__device__ __forceinline__ bool is_solid(const World& w, int x, int y, int z) {
+    uint64_t b = brick_of(w, x >> 3, y >> 3, z >> 3);
+    uint32_t local = (uint32_t)(x & 7) | ((uint32_t)(y & 7) << 3) | ((uint32_t)(z & 7) << 6);
+    uint32_t word = w.brick[b * 32 + (local >> 5)];
+    return (word >> (local & 31)) & 1u;
+}
+
+// CSDF byte of an in-range coarse cell.
+__device__ __forceinline__ uint32_t csdf_at(const World& w, int cx, int cy, int cz) {
+    uint64_t b = brick_of(w, cx >> 2, cy >> 2, cz >> 2);
+    uint32_t local = (uint32_t)(cx & 3) | ((uint32_t)(cy & 3) << 2) | ((uint32_t)(cz & 3) << 4);
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(w.brick) + b * 128 + 64 + local;
+    return *p;
+}
+
+// getDistance(float3) (include/raytracing_functions.cuh:35-51): truncating
+// cast after floorf*0.5, clamped to the grid (Appendix R11).
+__device__ __forceinline__ float get_distance_f(const World& w, f3 p) {
+    int cx = (int)(floorf(p.x) * 0.5f);
+    int cy = (int)(floorf(p.y) * 0.5f);
+    int cz = (int)(floorf(p.z) * 0.5f);
+    cx = max(min(cx, w.SX - 1), 0);
+    cy = max(min(cy, w.SY - 1), 0);
+    cz = max(min(cz, w.SZ - 1), 0);
+    return (float)csdf_at(w, cx, cy, cz);
+}
+
+// getDistance(int3) (include/raytracing_functions.cuh:52-67).
+__device__ __forceinline__ uint32_t get_distance_i(const World& w, int x, int y, int z) {
+    int cx = x / 2, cy = y / 2, cz = z / 2;
+    cx = max(min(cx, w.SX - 1), 0);
+    cy = max(min(cy, w.SY - 1), 0);
+    cz = max(min(cz, w.SZ - 1), 0);
+    return csdf_at(w, cx, cy, cz);
+}
+
+// ---------------------------------------------------------------- noise
+// include/TerrainGeneration.cuh:25-44
+__device__ __forceinline__ uint32_t hash3(int xi, int yi, int zi) {
+    uint32_t key = (uint32_t)xi * 73856093u;
+    key ^= (uint32_t)yi * 19349663u;
+    key ^= (uint32_t)zi * 83492791u;
+    key = (key ^ 61u) ^ (key >> 16);
+    key *= 9u;
+    key = key ^ (key >> 4);
+    key *= 0x27d4eb2du;
+    key = key ^ (key >> 15);
+    return key;
+}
+__device__ __forceinline__ uint32_t hash2(int xi, int yi) {
+    uint32_t key = (uint32_t)xi * 73856093u;
+    key ^= (uint32_t)yi * 19349663u;
+    key = (key ^ 61u) ^ (key >> 16);
+    key *= 9u;
+    key = key ^ (key >> 4);
+    key *= 0x27d4eb2du;
+    key = key ^ (key >> 15);
+    return key;
+}
+
+// gradient dot product: include/TerrainGeneration.cuh:161-175 + :156-158
+__device__ __forceinline__ float grad_dot3(uint32_t h, float x, float y, float z) {
+    h &= 15u;
+    float gx = (h & 1u) ? 1.0f : -1.0f;
+    float gy = (h & 2u) ? 1.0f : -1.0f;
+    float gz = (h & 4u) ? 1.0f : -1.0f;
+    if (h < 8u) gz = 0.0f; else if (h < 12u) gx = 0.0f; else gy = 0.0f;
+    return gx * x + gy * y + gz * z;
+}
+
+// include/TerrainGeneration.cuh:178-254
+__device__ __forceinline__ float simplex3D(float px, float py, float pz) {
+    const float F3 = 1.0f / 3.0f;
+    float s = (px + py + pz) * F3;
+    int i = (int)floorf(px + s), j = (int)floorf(py + s), k = (int)floorf(pz + s);
+    const float G3 = 1.0f / 6.0f;
+    float t = (float)(i + j + k) * G3;
+    float x0 = px - ((float)i - t), y0 = py - ((float)j - t), z0 = pz - ((float)k - t);
+    int c_xy = x0 >= y0, c_xz = x0 >= z0, c_yz = y0 >= z0;
+    int i1 = c_xy & c_xz, j1 = (1 - c_xy) & c_yz, k1 = (1 - c_xz) & (1 - c_yz);
+    int i2 = 1 - ((1 - c_xy) & (1 - c_xz));
+    int j2 = 1 - (c_xy & (1 - c_yz));
+    int k2 = 1 - (c_xz & c_yz);
+    float x1 = x0 - (float)i1 + G3, y1 = y0 - (float)j1 + G3, z1 = z0 - (float)k1 + G3;
+    float x2 = x0 - (float)i2 + 2.0f * G3, y2 = y0 - (float)j2 + 2.0f * G3, z2 = z0 - (float)k2 + 2.0f * G3;
+    float x3 = x0 - 1.0f + 3.0f * G3, y3 = y0 - 1.0f + 3.0f * G3, z3 = z0 - 1.0f + 3.0f * G3;
+    float t0 = 0.5f - x0 * x0 - y0 * y0 - z0 * z0; t0 = fmaxf(0.0f, t0); t0 *= t0;
+    float n0 = t0 * t0 * grad_dot3(hash3(i, j, k), x0, y0, z0);
+    float t1 = 0.5f - x1 * x1 - y1 * y1 - z1 * z1; t1 = fmaxf(0.0f, t1); t1 *= t1;
+    float n1 = t1 * t1 * grad_dot3(hash3(i + i1, j + j1, k + k1), x1, y1, z1);
+    float t2 = 0.5f - x2 * x2 - y2 * y2 - z2 * z2; t2 = fmaxf(0.0f, t2); t2 *= t2;
+    float n2 = t2 * t2 * grad_dot3(hash3(i + i2, j + j2, k + k2), x2, y2, z2);
+    float t3 = 0.5f - x3 * x3 - y3 * y3 - z3 * z3; t3 = fmaxf(0.0f, t3); t3 *= t3;
+    float n3 = t3 * t3 * grad_dot3(hash3(i + 1, j + 1, k + 1), x3, y3, z3);
+    return 96.0f * (n0 + n1 + n2 + n3);
+}
+
+// include/TerrainGeneration.cuh:65-142 (G2 as written: (3-sqrt3)*0.5)
+__device__ __forceinline__ float simplex2D(float px, float py) {
+    const float F2 = (sqrtf(3.0f) - 1.0f) * 0.5f;
+    const float G2 = (3.0f - sqrtf(3.0f)) * 0.5f;
+    float s = (px + py) * F2;
+    int i = (int)floorf(px + s), j = (int)floorf(py + s);
+    float t = (float)(i + j) * G2;
+    float x0 = px - (float)i + t, y0 = py - (float)j + t;
+    int i1 = x0 > y0 ? 1 : 0, j1 = 1 - i1;
+    float x1 = x0 - (float)i1 + G2, y1 = y0 - (float)j1 + G2;
+    float x2 = x0 - 1.0f + 2.0f * G2, y2 = y0 - 1.0f + 2.0f * G2;
+    float n = 0.0f;
+    float tt[3] = {0.5f - x0 * x0 - y0 * y0, 0.5f - x1 * x1 - y1 * y1, 0.5f - x2 * x2 - y2 * y2};
+    uint32_t hh[3] = {hash2(i, j), hash2(i + i1, j + j1), hash2(i + 1, j + 1)};
+    float xs[3] = {x0, x1, x2}, ys[3] = {y0, y1, y2};
+    float nn[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint32_t h = hh[q] & 7u;
+        float gx = (h & 1u) ? 1.0f : -1.0f, gy = (h & 2u) ? 1.0f : -1.0f;
+        if (h < 4u) gy = 0.0f; else gx = 0.0f;
+        float tq = fmaxf(0.0f, tt[q]); tq *= tq;
+        nn[q] = tq * tq * (gx * xs[q] + gy * ys[q]);
+    }
+    n = nn[0] + nn[1] + nn[2];
+    return 70.0f * n;
+}
+
+// include/TerrainGeneration.cuh:259-268
+__device__ __forceinline__ float fbm3D(float x, float y, float z, int oct, float freq, float lac, float pers) {
+    float total = 0.0f, amp = 1.0f;
+    for (int i = 0; i < oct; i++) {
+        total += simplex3D(x * freq, y * freq, z * freq) * amp;
+        freq *= lac;
+        amp *= pers;
+    }
+    return total;
+}
+
+// include/TerrainGeneration.cuh:284-356 (float abs on the cave noise: R8)
+__device__ __forceinline__ float evaluate(float x, float y, float z) {
+    if (y <= 30.0f) return 100.0f;
+    float biome = (simplex2D(x * 0.005f, z * 0.005f) + 1.0f) * 0.5f;
+    float amp = 60.0f + biome * (400.0f - 60.0f);
+    float density = 10.0f - y;
+    float surf = fbm3D(x, y, z, 7, 0.002f, 2.1f, 0.45f);
+    density += surf * amp;
+    if (density > 0.0f) {
+        float cave_raw = fbm3D(x + 123.456f, y, z, 3, 0.009f, 2.1f, 0.45f);
+        float cave_norm = (cave_raw + 1.0f) * 0.5f;
+        bool spaghetti = fabsf(cave_raw) < 0.025f;
+        float region = (simplex3D(x * 0.006f, y * 0.006f, z * 0.006f) + 1.0f) * 0.5f;
+        bool cavern = (region > 0.65f) && (cave_norm < 0.3f);
+        if (spaghetti || cavern) density -= 2.0f;
+    }
+    return density;
+}
+
+// ---------------------------------------------------------------- traversal
+// Device hit record.  Layout of the first 36 B mirrors the reference's
+// hitInfo (include/raytracing_functions.cuh:14-21): pos, normal, half2 uv,
+// bool hit, int its; uv is carried here as two half-exact floats.
+struct Hit {
+    f3 pos, normal;
+    float u, v;
+    bool hit;
+    bool undef;      // reference mask==-128 hit (Appendix R2)
+    int its;
+};
+
+struct StepCount {  // per-trace work counters (algorithmic bytes)
+    uint32_t sphere, dda, check;
+};
+
+// approximateCSDF (src/raytracing_functions.cu:65-83).  Inside the bounds
+// check the coarse index is in range, so no clamp is needed.
+template <bool COUNT>
+__device__ __forceinline__ f3 approximate_csdf(const World& w, f3 pos, f3 dir, StepCount& sc) {
+    for (int it = 0; it < 100; it++) {
+        if (pos.x < 0 || pos.y < 0 || pos.z < 0 || pos.x >= w.fX || pos.y >= w.fY || pos.z >= w.fZ)
+            return V(-100.0f, -100.0f, -100.0f);
+        int cx = (int)(floorf(pos.x) * 0.5f);
+        int cy = (int)(floorf(pos.y) * 0.5f);
+        int cz = (int)(floorf(pos.z) * 0.5f);
+        float d = (float)csdf_at(w, cx, cy, cz);
+        if (COUNT) sc.sphere++;
+        if (d <= 1.0f) return pos;
+        pos = add(pos, scale(dir, d));
+    }
+    return pos;
+}
+
+// trace (src/raytracing_functions.cu:85-202).  dist_h is the already
+// half-rounded start distance (the reference's `half distance`).
+template <bool COUNT>
+__device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
+    Hit H;
+    H.hit = false; H.undef = false; H.its = 0;
+    H.pos = V(-500.0f, -500.0f, -500.0f);
+    H.normal = V(0.0f, 0.0f, 0.0f);
+    H.u = 0.0f; H.v = 0.0f;
+    f3 cur = add(cam, scale(dir, dist_h));
+    const float ddx = dir.x != 0 ? fabsf(1.0f / dir.x) : 1e10f;
+    const float ddy = dir.y != 0 ? fabsf(1.0f / dir.y) : 1e10f;
+    const float ddz = dir.z != 0 ? fabsf(1.0f / dir.z) : 1e10f;
+    const int sx = (dir.x > 0) - (dir.x < 0);
+    const int sy = (dir.y > 0) - (dir.y < 0);
+    const int sz = (dir.z > 0) - (dir.z < 0);
+    for (int major = 0; major < 5; major++) {
+        cur = approximate_csdf<COUNT>(w, cur, dir, sc);
+        int ix = (int)floorf(cur.x), iy = (int)floorf(cur.y), iz = (int)floorf(cur.z);
+        float tx = ((sx > 0) ? ((float)ix + 1.0f - cur.x) : (cur.x - (float)ix)) * ddx;
+        float ty = ((sy > 0) ? ((float)iy + 1.0f - cur.y) : (cur.y - (float)iy)) * ddy;
+        float tz = ((sz > 0) ? ((float)iz + 1.0f - cur.z) : (cur.z - (float)iz)) * ddz;
+        int mask = -128;
+        bool jumped = false;
+        for (int i = 0; i < 200; i++) {
+            if ((i & 7) == 7) {
+                uint32_t d = get_distance_i(w, ix, iy, iz);
+                if (COUNT) sc.check++;
+                if (d > 2) {
+                    f3 c = V((float)ix + 0.5f, (float)iy + 0.5f, (float)iz + 0.5f);
+                    float t = dot(sub(c, cur), dir);
+                    f3 por = add(cur, scale(dir, t));
+                    cur = add(por, scale(dir, (float)d * 2.0f));
+                    jumped = true;
+                    break;
+                }
+            }
+            if (ix < 0 || iy < 0 || iz < 0 || ix >= w.X || iy >= w.Y || iz >= w.Z) return H;
+            if (COUNT) sc.dda++;
+            if (is_solid(w, ix, iy, iz)) {
+                H.hit = true;
+                if (mask == 0) {
+                    H.normal = V((float)-sx, 0.0f, 0.0f);
+                    H.pos = add(cur, scale(dir, tx - ddx));
+                    H.u = hround(H.pos.y - (float)iy);
+                    H.v = hround(H.pos.z - (float)iz);
+                    if (sx == -1) H.v = hround(1.0f - H.v);
+                } else if (mask == 1) {
+                    H.normal = V(0.0f, (float)-sy, 0.0f);
+                    H.pos = add(cur, scale(dir, ty - ddy));
+                    H.u = hround(H.pos.x - (float)ix);
+                    H.v = hround(H.pos.z - (float)iz);
+                } else if (mask == 2) {
+                    H.normal = V(0.0f, 0.0f, (float)-sz);
+                    H.pos = add(cur, scale(dir, tz - ddz));
+                    H.u = hround(H.pos.x - (float)ix);
+                    H.v = hround(H.pos.y - (float)iy);
+                    if (sz == 1) H.u = hround(1.0f - H.u);
+                } else {
+                    H.undef = true;   // Appendix R2
+                }
+                return H;
+            }
+            if (tx < ty) {
+                if (tx < tz) { tx += ddx; ix += sx; mask = 0; }
+                else         { tz += ddz; iz += sz; mask = 2; }
+            } else {
+                if (ty < tz) { ty += ddy; iy += sy; mask = 1; }
+                else         { tz += ddz; iz += sz; mask = 2; }
+            }
+        }
+        if (jumped) continue;
+        break;   // 200 DDA steps without hit or jump: miss
+    }
+    return H;
+}
+
+// tanf(0.4f), correctly rounded (see oracle OR_TAN_CONE).
+#define RV_TAN_CONE 0.42279321873816174f
+
+// traceCone (src/raytracing_functions.cu:212-273)
+template <bool COUNT>
+__device__ __forceinline__ f3 trace_cone(const World& w, f3 pos, f3 dir, uint32_t& steps) {
+    f3 acc = V(0.0f, 0.0f, 0.0f);
+    float alpha = 0.0f;
+    float cd = 1.5f * 2.0f;
+    for (int i = 0; i < 20; ++i) {
+        if (alpha > 0.99f || cd > 64.0f) break;
+        if (COUNT) steps++;
+        f3 p = add(pos, scale(dir, cd));
+        float scene = get_distance_f(w, p) * 2.0f;
+        float width = cd * RV_TAN_CONE;
+        if (scene < width) { alpha = 1.0f; continue; }
+        int gx = (int)(floorf(p.x) / 4.0f);
+        int gy = (int)(floorf(p.y) / 4.0f);
+        int gz = (int)(floorf(p.z) / 4.0f);
+        if (gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ) {
+            uint32_t s = w.gi[(uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx];
+            f3 c = V((float)(s & 255u) / 255.0f, (float)((s >> 8) & 255u) / 255.0f,
+                     (float)((s >> 16) & 255u) / 255.0f);
+            float a = (float)(s >> 24) / 255.0f;
+            float blend = (1.0f - alpha) * a;
+            acc = add(acc, scale(c, blend));
+            alpha += blend;
+        }
+        cd += fmaxf(1.5f, width * 0.5f);
+    }
+    return acc;
+}
+
+// sampleSky (src/raytracing_functions.cu:10-26)
+__device__ __forceinline__ f3 sample_sky(f3 dir, f3 sun) {
+    if (dot(dir, sun) > 0.999f) return V(1.0f * 10.0f, 0.9f * 10.0f, 0.2f * 10.0f);
+    float t = clampf(0.5f * (dir.y + 1.0f), 0.0f, 1.0f);
+    return lerp(V(0.2f, 0.4f, 0.8f), V(0.6f, 0.8f, 1.0f), t);
+}
+
+// sampleTexture (src/raytracing_functions.cu:28-62): fp16 UV math, the
+// +121.3 offsets added in double (:43), swapped atlas coords (R10),
+// point filter + wrap on a 256x256 RGBA8 atlas, texel = byte/255.
+__device__ __forceinline__ f3 sample_texture(const World& w, float u, float v, f3 pos) {
+    const float freq = 0.05f;
+    float e = simplex3D(floorf(pos.x) * freq, floorf(pos.y) * freq, floorf(pos.z) * freq);
+    float e2 = simplex3D(floorf((float)((double)pos.x + 121.3)) * freq * 0.3f,
+                         floorf((float)((double)pos.y + 1321.3)) * freq * 0.3f,
+                         floorf((float)((double)pos.z + 721.5)) * freq * 0.3f);
+    e = e * 0.4f + e2 * 0.6f;
+    int tile;  // (bx,by) in 1/16 units
+    if (e < -1.3f) tile = 0x10;        // stone   (0,1)
+    else if (e < -1.2f) tile = 0x23;   // diamond (3,2)
+    else if (e < -0.7f) tile = 0x12;   // iron    (2,1)
+    else if (e < 0.0f) tile = 0x10;    // stone
+    else if (e < 0.1f) tile = 0x22;    // coal    (2,2)
+    else if (e < 0.4f) tile = 0x01;    // cobble  (1,0)
+    else if (e < 0.8f) tile = 0x20;    // dirt    (0,2)
+    else if (e < 1.2f) tile = 0x00;    // stone2  (0,0)
+    else tile = 0x10;                  // stone
+    float bx = (float)(tile & 15) * (1.0f / 16.0f), by = (float)(tile >> 4) * (1.0f / 16.0f);
+    float ux = hround(hround(u * 0.0625f) + bx);
+    float uy = hround(hround(v * 0.0625f) + by);
+    float cu = uy - floorf(uy), cv = ux - floorf(ux);
+    int col = min((int)floorf(cu * (float)w.aw), w.aw - 1);
+    int row = min((int)floorf(cv * (float)w.ah), w.ah - 1);
+    uint32_t t = w.atlas[row * w.aw + col];
+    return V((float)(t & 255u) / 255.0f, (float)((t >> 8) & 255u) / 255.0f,
+             (float)((t >> 16) & 255u) / 255.0f);
+}
+
+}  // namespace rv

@@ -1,0 +1,57 @@
+// rv_internal.h -- types shared by the kernels (rv_kernels.hip) and the
+// C-ABI host layer (rv_abi.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rvgrt.h"
+#include "rv_device.h"
+
+namespace rv {
+
+// counter slots; order == rv_stats field order
+enum {
+    CNT_TRACES = 0, CNT_PRIMARY, CNT_SHADOW, CNT_REFL, CNT_REFL_SHADOW, CNT_PP_PRIMARY, CNT_PP_SHADOW,
+    CNT_CONES, CNT_CONE_STEPS, CNT_SPHERE, CNT_DDA, CNT_CHECK, CNT_TEX, CNT_UNDEF, CNT_GI_TRACES,
+    CNT_FRAMES, NCNT
+};
+
+struct FrameParams {
+    f3 pos, fo, ri, up, sun;
+    float time, jx, jy;
+    float vp[16], pvp[16];
+    int W, H, hw, hh, flags;
+    uint32_t* color; size_t color_pitch;
+    uint32_t* mv; size_t mv_pitch;
+    uint16_t* depth; size_t depth_pitch;
+    float* hdist; float* hshadow;
+    unsigned long long* counters;
+    const int* tiles; int ntiles; int tile_px; int tiles_x;
+    uint32_t* tilebuf;
+};
+
+struct RvHitDev {   // == rv_hit
+    float pos[3], normal[3], u, v;
+    int hit, undef, sphere, dda, check, pad;
+};
+static_assert(sizeof(RvHitDev) == sizeof(rv_hit), "rv_hit layout");
+
+void launch_fill_bricks(hipStream_t s, uint32_t* brick, const World& w, int sx, int sz);
+void launch_csdf(hipStream_t s, uint32_t* brick, const World& w, uint8_t* t0, uint8_t* t1);
+void launch_bits_import(hipStream_t s, const uint32_t* canon, uint32_t* brick, const World& w, int lx, int ly);
+void launch_bits_export(hipStream_t s, const uint32_t* brick, uint32_t* canon, const World& w, int lx, int ly);
+void launch_csdf_import(hipStream_t s, const uint8_t* canon, uint32_t* brick, const World& w);
+void launch_csdf_export(hipStream_t s, const uint32_t* brick, uint8_t* canon, const World& w);
+void launch_gi_init(hipStream_t s, uint32_t* gi, const World& w, f3 sun, unsigned long long* counters);
+void launch_gi_update(hipStream_t s, const uint32_t* prev, uint32_t* next, const World& w, f3 sun,
+                      uint32_t frame, uint64_t first, uint64_t count, unsigned long long* counters);
+void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
+void launch_render(hipStream_t s, const World& w, const FrameParams& f);
+void launch_prepass_tiles(hipStream_t s, const World& w, const FrameParams& f);
+void launch_render_tiles(hipStream_t s, const World& w, const FrameParams& f);
+void launch_untile(hipStream_t s, const uint32_t* tiles, const int* ids, int ntiles, int tile_px, int tiles_x,
+                   int W, int H, uint32_t* color, size_t pitch);
+void launch_trace_rays(hipStream_t s, const World& w, const float* org, const float* dir, const float* dist,
+                       int64_t n, RvHitDev* out);
+
+}  // namespace rv

@@ -1,0 +1,224 @@
+"""Host-side mirror of the reference's StateRender interface over the C ABI.
+
+Reference: class StateRender (include/StateRender.cuh:11-47), its
+drawCUDA (src/StateRender.cu:289-346), CoarseArray::InitializeGIData /
+UpdateGIData (src/CoarseArray.cu:357-395) and the init sequence of
+State::Create (src/State.cpp:24-56).  Every method forwards to
+librvgrt_hip.so; errors raise RvError with rv_last_error().
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import RvError, rv_camera, rv_config, rv_hit, rv_stats
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def camera_from_pose(pos, yaw, pitch, width, height):
+    """Character::Update basis + unjittered VP (src/Character.cpp:18-126)."""
+    L = _lib.load()
+    cam = rv_camera()
+    vp = np.zeros(16, np.float32)
+    st = L.rv_camera_from_pose(float(pos[0]), float(pos[1]), float(pos[2]), float(yaw),
+                               float(pitch), int(width), int(height), C.byref(cam), _ptr(vp))
+    if st != 0:
+        raise RvError(f"rv_camera_from_pose: {_lib.STATUS_NAMES.get(st, st)}")
+    return cam, vp
+
+
+def camera_dict(cam: rv_camera, vp):
+    return {"pos": np.array(cam.pos[:], np.float32), "fo": np.array(cam.forward[:], np.float32),
+            "ri": np.array(cam.right[:], np.float32), "up": np.array(cam.up[:], np.float32),
+            "vp": np.asarray(vp, np.float32)}
+
+
+class StateRender:
+    """One render context on one GPU (reference: StateRender + its arrays)."""
+
+    def __init__(self, log2_dims=(9, 9, 9), width=1920, height=1080, flags=_lib.RV_FLAGS_REFERENCE,
+                 atlas=None, device=0, seed=(0, 0), ref_compat=True, ref_oob_jy=0.0,
+                 gi_rays_per_frame=0):
+        self._L = _lib.load()
+        self.width, self.height = int(width), int(height)
+        self.log2_dims = tuple(int(v) for v in log2_dims)
+        self.flags = int(flags)
+        self._atlas = None if atlas is None else np.ascontiguousarray(atlas, np.uint8)
+        cfg = rv_config()
+        cfg.log2_x, cfg.log2_y, cfg.log2_z = self.log2_dims
+        cfg.width, cfg.height, cfg.flags = self.width, self.height, self.flags
+        cfg.seed_x, cfg.seed_z = int(seed[0]), int(seed[1])
+        cfg.ref_compat, cfg.ref_oob_jy = int(bool(ref_compat)), float(ref_oob_jy)
+        if self._atlas is not None:
+            cfg.atlas_rgba8 = self._atlas.ctypes.data
+            cfg.atlas_h, cfg.atlas_w = self._atlas.shape[0], self._atlas.shape[1]
+        cfg.gi_rays_per_frame = int(gi_rays_per_frame)
+        h = C.c_void_p()
+        st = self._L.rv_create(C.byref(cfg), int(device), C.byref(h))
+        if st != 0:
+            raise RvError(f"rv_create failed: {_lib.STATUS_NAMES.get(st, st)} "
+                          "(needs a gfx950 GPU and a valid config)")
+        self._h = h
+        X, Y, Z = (1 << d for d in self.log2_dims)
+        self.dims = (X, Y, Z)
+
+    # ------------------------------------------------------------ plumbing
+    def _check(self, st, what):
+        if st != 0:
+            msg = self._L.rv_last_error(self._h)
+            raise RvError(f"{what}: {_lib.STATUS_NAMES.get(st, st)}: "
+                          f"{msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int):
+        self._check(self._L.rv_set_stream(self._h, C.c_void_p(stream_handle)), "rv_set_stream")
+
+    def sync(self):
+        self._check(self._L.rv_sync(self._h), "rv_sync")
+
+    # ------------------------------------------------------------ world
+    def world_build(self):
+        """State::Create: CArray::fill -> GenerateSDF -> InitializeGIData."""
+        self._check(self._L.rv_world_build(self._h), "rv_world_build")
+
+    def csdf_build(self):
+        self._check(self._L.rv_csdf_build(self._h), "rv_csdf_build")
+
+    def gi_init(self):
+        self._check(self._L.rv_gi_init(self._h), "rv_gi_init")
+
+    def gi_update(self, frame, first=0, count=None):
+        if count is None:
+            X, Y, Z = self.dims
+            count = (X // 4) * (Y // 4) * (Z // 4)
+        self._check(self._L.rv_gi_update(self._h, int(frame), int(first), int(count)), "rv_gi_update")
+
+    def gi_sweeps(self, n):
+        for s in range(n):
+            self.gi_update(s)
+
+    def update_gi_data(self):
+        """CoarseArray::UpdateGIData: RAYPS cells, rolling offset."""
+        self._check(self._L.rv_update_gi_data(self._h), "rv_update_gi_data")
+
+    def world_import(self, kind, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        self._check(self._L.rv_world_import(self._h, kind, _ptr(a), a.nbytes), "rv_world_import")
+
+    def world_export(self, kind) -> np.ndarray:
+        X, Y, Z = self.dims
+        if kind == _lib.RV_WORLD_BITS:
+            a = np.zeros(X * Y * Z // 32, np.uint32)
+        elif kind == _lib.RV_WORLD_CSDF:
+            a = np.zeros(X * Y * Z // 8, np.uint8)
+        else:
+            a = np.zeros((X // 4) * (Y // 4) * (Z // 4) * 4, np.uint8)
+        self._check(self._L.rv_world_export(self._h, kind, _ptr(a), a.nbytes), "rv_world_export")
+        return a
+
+    # ------------------------------------------------------------ frames
+    def draw_cuda(self, pos, fo, up, ri, vp, prev_vp, jitter_x=0.0, jitter_y=0.0):
+        """StateRender::drawCUDA, same argument order."""
+        arrs = [np.ascontiguousarray(a, np.float32) for a in (pos, fo, up, ri, vp, prev_vp)]
+        self._check(self._L.rv_draw_cuda(self._h, *[_ptr(a) for a in arrs],
+                                         float(jitter_x), float(jitter_y)), "rv_draw_cuda")
+
+    def frame(self, cam: rv_camera, vp, prev_vp=None, time=0.0, jx=0.0, jy=0.0, flags=None):
+        vp = np.ascontiguousarray(vp, np.float32)
+        pvp = vp if prev_vp is None else np.ascontiguousarray(prev_vp, np.float32)
+        f = self.flags if flags is None else int(flags)
+        self._check(self._L.rv_frame(self._h, C.byref(cam), _ptr(vp), _ptr(pvp), float(time),
+                                     float(jx), float(jy), f), "rv_frame")
+
+    def frame_tiles(self, cam, vp, tile_ids, tile_px=64, prev_vp=None, time=0.0, jx=0.0, jy=0.0,
+                    flags=None):
+        vp = np.ascontiguousarray(vp, np.float32)
+        pvp = vp if prev_vp is None else np.ascontiguousarray(prev_vp, np.float32)
+        ids = np.ascontiguousarray(tile_ids, np.int32)
+        f = self.flags if flags is None else int(flags)
+        self._check(self._L.rv_frame_tiles(self._h, C.byref(cam), _ptr(vp), _ptr(pvp), float(time),
+                                           float(jx), float(jy), f, _ptr(ids), len(ids),
+                                           int(tile_px)), "rv_frame_tiles")
+
+    def tile_buffer(self):
+        p, n = C.c_void_p(), C.c_size_t()
+        self._check(self._L.rv_tile_buffer(self._h, C.byref(p), C.byref(n)), "rv_tile_buffer")
+        return p.value, n.value
+
+    def bind_tile_buffer(self, dev_ptr, nbytes):
+        self._check(self._L.rv_bind_tile_buffer(self._h, C.c_void_p(dev_ptr), int(nbytes)),
+                    "rv_bind_tile_buffer")
+
+    def untile(self, dev_ptr: int, tile_ids, tile_px=64):
+        ids = np.ascontiguousarray(tile_ids, np.int32)
+        self._check(self._L.rv_untile(self._h, C.c_void_p(dev_ptr), _ptr(ids), len(ids), int(tile_px)),
+                    "rv_untile")
+
+    def bind_output(self, kind, dev_ptr, pitch):
+        self._check(self._L.rv_bind_output(self._h, kind, C.c_void_p(dev_ptr), pitch), "rv_bind_output")
+
+    def image_ptr(self, kind):
+        p, pitch = C.c_void_p(), C.c_size_t()
+        self._check(self._L.rv_image_ptr(self._h, kind, C.byref(p), C.byref(pitch)), "rv_image_ptr")
+        return p.value, pitch.value
+
+    def readback(self, kind=_lib.RV_IMAGE_COLOR) -> np.ndarray:
+        W, H = self.width, self.height
+        if kind == _lib.RV_IMAGE_COLOR:
+            a = np.zeros((H, W, 4), np.uint8)
+        elif kind == _lib.RV_IMAGE_MOTION:
+            a = np.zeros((H, W, 2), np.uint16)
+        elif kind == _lib.RV_IMAGE_DEPTH:
+            a = np.zeros((H, W), np.uint16)
+        else:
+            a = np.zeros((H // 2, W // 2), np.float32)
+        self._check(self._L.rv_readback(self._h, kind, _ptr(a), 0), "rv_readback")
+        return a
+
+    # ------------------------------------------------------------ test surface
+    def trace_rays(self, org, dirs, dist) -> np.ndarray:
+        org = np.ascontiguousarray(org, np.float32)
+        dirs = np.ascontiguousarray(dirs, np.float32)
+        dist = np.ascontiguousarray(dist, np.float32)
+        n = len(dist)
+        out = (rv_hit * max(n, 1))()
+        self._check(self._L.rv_trace_rays(self._h, _ptr(org), _ptr(dirs), _ptr(dist), n,
+                                          C.cast(out, C.c_void_p)), "rv_trace_rays")
+        dt = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("u", "<f4"), ("v", "<f4"),
+                       ("hit", "<i4"), ("undef", "<i4"), ("sphere_steps", "<i4"),
+                       ("dda_steps", "<i4"), ("csdf_checks", "<i4"), ("pad", "<i4")])
+        return np.frombuffer(bytes(out), dt, count=n).copy()
+
+    def stats(self, stage=-1) -> dict:
+        """Counters (RV_F_STATS frames): stage -1 all, 0 non-pre-pass, 1 pre-pass."""
+        s = rv_stats()
+        self._check(self._L.rv_stats_stage(self._h, int(stage), C.byref(s)), "rv_stats_stage")
+        return s.as_dict()
+
+    def timing_enable(self, max_frames):
+        self._check(self._L.rv_timing_enable(self._h, int(max_frames)), "rv_timing_enable")
+
+    def timing_get(self):
+        """(ms per stage [gi, prepass, render] summed over frames, frames)."""
+        ms = (C.c_double * 3)()
+        n = C.c_int32()
+        self._check(self._L.rv_timing_get(self._h, ms, C.byref(n)), "rv_timing_get")
+        return list(ms), n.value
+
+    def stats_reset(self):
+        self._check(self._L.rv_stats_reset(self._h), "rv_stats_reset")

@@ -1,0 +1,30 @@
+#!/usr/bin/env bash
+# Runs GPU steps on the gpurun box, each under its own time limit.  Stops at
+# the first step that crashes, faults or times out (exit >= 2 for pytest,
+# non-zero otherwise); ordinary pytest test failures (exit 1) continue.
+#   usage: tools/gpu_run.sh step1 step2 ...   (steps: smoke tests bench prof)
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+run() {  # name limit cmd...
+    local name=$1 lim=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 5 "gpurun_out/$name.log"
+    return $rc
+}
+for step in "$@"; do
+    case $step in
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
+        tests) run tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+               rc=$?; [ $rc -le 1 ] || exit 3 ;;
+        bench) run bench 600 python bench.py || exit 3 ;;
+        bench_c3) run bench_c3 600 python bench.py --config c3 --cpu-seconds 5 || exit 3 ;;
+        bench_c4) run bench_c4 600 python bench.py --config c4 --cpu-seconds 0 --steps 10 || exit 3 ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
+                  -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 || exit 3 ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
