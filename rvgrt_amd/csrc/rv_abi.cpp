@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -45,6 +46,8 @@ struct rv_ctx {
     uint32_t gi_frame = 0;
     uint64_t gi_offset = 0;
     bool world_ready = false;
+    int sched = SCHED_CHUNK;
+    unsigned* queue = nullptr;   // work counters for SCHED_QUEUE
     std::string err;
 };
 
@@ -165,6 +168,9 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (hipMalloc(&c->hshadow, hbytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "halfshadow");
     hipMemset(c->hdist, 0, hbytes);
     hipMemset(c->hshadow, 0, hbytes);
+    if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
+    if (hipMalloc(&c->queue, 16) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "queue");
+    hipMemset(c->queue, 0, 16);
     if (hipMalloc(&c->counters, 2 * NCNT * sizeof(unsigned long long)) != hipSuccess)
         return cleanup_fail(RV_ERR_OOM, "counters");
     hipMemset(c->counters, 0, 2 * NCNT * sizeof(unsigned long long));
@@ -180,7 +186,7 @@ void rv_destroy(rv_ctx* c) {
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
     hipFree(c->own_color); hipFree(c->own_mv); hipFree(c->own_depth);
     hipFree(c->hdist); hipFree(c->hshadow); hipFree(c->counters);
-    hipFree(c->tile_ids); hipFree(c->tilebuf);
+    hipFree(c->tile_ids); hipFree(c->tilebuf); hipFree(c->queue);
     for (hipEvent_t e : c->ev) hipEventDestroy(e);
     delete c;
 }
@@ -344,6 +350,8 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
     f.depth = c->depth; f.depth_pitch = c->depth_pitch;
     f.hdist = c->hdist; f.hshadow = c->hshadow;
     f.counters = c->counters;
+    f.sched = c->sched;
+    f.queue = c->queue;
     return f;
 }
 
@@ -352,6 +360,7 @@ static rv_status run_stages(rv_ctx* c, const FrameParams& f, bool tiles) {
     bool timed = c->timing_n < c->timing_cap;
     hipEvent_t* e = timed ? &c->ev[4 * c->timing_n] : nullptr;
     World w = current_world(c);
+    if (c->sched == SCHED_QUEUE) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 16, c->stream));
     if (timed) {
         if (!c->gi_pending) HIP_TRY(c, hipEventRecord(e[0], c->stream));
         HIP_TRY(c, hipEventRecord(e[1], c->stream));

@@ -16,7 +16,12 @@ enum {
     CNT_FRAMES, NCNT
 };
 
+// workgroup -> pixel-block scheduling of the frame kernels (see rv_kernels.hip)
+enum { SCHED_IDENTITY = 0, SCHED_BAND = 1, SCHED_CHUNK = 2, SCHED_QUEUE = 3 };
+
 struct FrameParams {
+    int sched;
+    unsigned* queue;   // [0] pre-pass, [1] render work counters (SCHED_QUEUE)
     f3 pos, fo, ri, up, sun;
     float time, jx, jy;
     float vp[16], pvp[16];
