@@ -50,6 +50,15 @@ CONFIGS = {
                        "2048^3 world, 3840x2160, 2-bounce GI + reflections, tile-parallel"),
 }
 
+# Poses for the small (128^3) parity worlds: the C1-C5 pose rule puts the
+# camera inside the mountains at the world's low-x/low-z corner there, so the
+# small-world tests look back at them from the open water side instead.
+TEST_POSES_128 = {
+    "P0": ((110.0, 70.0, 120.0), 2.44, -3.4415927),   # mountains, water, sky
+    "P1": ((64.0, 45.0, 120.0), 3.14, -3.2),          # water/reflection heavy
+}
+
+
 # float32 yaw/pitch exactly as the reference stores them (float members)
 def pose_f32(cfg: RenderConfig, which="P0"):
     import numpy as np

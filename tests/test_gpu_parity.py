@@ -105,11 +105,8 @@ def test_frame_parity(rv, atlas, oracle_world, oracle, name, flags, pose):
     W, H = 256, 144
     ow = oracle_world(lg, lg, lg, gi_sweeps=1)
     r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
-    n = 1 << lg
-    if pose == "P0":
-        pos, yaw, pitch = (0.1 * n, 0.6 * n, 0.1 * n), -0.7, -3.4415927
-    else:
-        pos, yaw, pitch = (0.1 * n, 60.0, 0.1 * n), -0.7, -3.7415927
+    from rvgrt_amd.configs import TEST_POSES_128
+    pos, yaw, pitch = TEST_POSES_128[pose]
     cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
     ocam = oracle.camera_from_pose(pos, yaw, pitch, W, H)
     for k in ("pos", "fo", "ri", "up", "vp"):   # host camera math agrees bit for bit
@@ -141,8 +138,8 @@ def test_frame_tiles_match_full_frame(rv, atlas, flags):
     lg = 7
     W, H = 256, 160
     r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
-    n = 1 << lg
-    cam, vp = rv.camera_from_pose((0.1 * n, 0.6 * n, 0.1 * n), -0.7, -3.4415927, W, H)
+    from rvgrt_amd.configs import TEST_POSES_128
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
     r.frame(cam, vp)
     full = r.readback(rv.RV_IMAGE_COLOR).copy()
     T = 32
@@ -173,8 +170,7 @@ def test_draw_cuda_ref_compat(rv, atlas):
     lg = 6
     W, H = 64, 48
     r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=7)
-    n = 1 << lg
-    cam, vp = rv.camera_from_pose((0.1 * n, 0.6 * n, 0.1 * n), -0.7, -3.4415927, W, H)
+    cam, vp = rv.camera_from_pose((60.0, 50.0, 60.0), 2.44, -3.4415927, W, H)
     d = rv.camera_dict(cam, vp)
     r.draw_cuda(d["pos"], d["fo"], d["up"], d["ri"], vp, vp, 0.3, 0.0)
     a = r.readback(rv.RV_IMAGE_COLOR).copy()
@@ -182,3 +178,31 @@ def test_draw_cuda_ref_compat(rv, atlas):
     b = r.readback(rv.RV_IMAGE_COLOR)
     assert np.array_equal(a, b)   # jitterX ignored, time = jitterY = 0
     r.close()
+
+
+def test_golden_fixtures(rv, atlas):
+    """World hashes and 256 traced rays from tests/golden (oracle-made), bit-exact."""
+    import hashlib
+    import json
+    import os
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    g = json.load(open(os.path.join(gdir, "golden.json")))
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    for lg in (6, 7):
+        r = rv.StateRender((lg, lg, lg), 64, 64, atlas=atlas)
+        r.world_build()
+        ref = g["worlds"][f"{1 << lg}^3"]
+        assert sha(r.world_export(rv.RV_WORLD_BITS)) == ref["bits"]
+        assert sha(r.world_export(rv.RV_WORLD_CSDF)) == ref["csdf"]
+        assert sha(r.world_export(rv.RV_WORLD_GI)) == ref["gi_init"]
+        r.gi_update(0)
+        assert sha(r.world_export(rv.RV_WORLD_GI)) == ref["gi_after_1_sweep"]
+        if lg == 7:
+            t = np.load(os.path.join(gdir, "traces_128.npz"))
+            h = r.trace_rays(t["org"], t["dir"], t["dist"])
+            assert np.array_equal(h["hit"], t["hit"]) and np.array_equal(h["undef"], t["undef"])
+            assert np.array_equal(h["pos"].view(np.uint32), t["pos"].view(np.uint32))
+            assert np.array_equal(h["normal"], t["normal"])
+            assert np.array_equal(h["u"], t["u"]) and np.array_equal(h["v"], t["v"])
+            assert np.array_equal(h["dda_steps"], t["n_dda"])
+        r.close()
