@@ -62,21 +62,36 @@ __device__ __forceinline__ uint64_t brick_of(const World& w, int bx, int by, int
     return (uint64_t)(uint32_t)bx | ((uint64_t)(uint32_t)by << w.lbx) | ((uint64_t)(uint32_t)bz << w.lbxy);
 }
 
+// Byte offset of brick record (bx,by,bz).  The brick array is < 4 GiB
+// (rv_create caps worlds at 2^34 voxels), so offsets stay 32-bit and loads
+// use the SGPR-base + 32-bit VGPR-offset form (no 64-bit address math).
+__device__ __forceinline__ uint32_t brick_byte(const World& w, uint32_t bx, uint32_t by, uint32_t bz) {
+    return (bx << 7) | (by << (w.lbx + 7)) | (bz << (w.lbxy + 7));
+}
+__device__ __forceinline__ uint32_t load_dword(const World& w, uint32_t byte_off) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + byte_off);
+}
+
+// Bit-word offset of voxel (x,y,z) and the bit inside it: within a brick
+// bit = (x&7) | (y&7)<<3 | (z&7)<<6, dword = bit>>5 = (y>>2 & 1) | (z&7)<<1.
+__device__ __forceinline__ uint32_t voxel_word_off(const World& w, uint32_t x, uint32_t y, uint32_t z) {
+    return brick_byte(w, x >> 3, y >> 3, z >> 3) | ((y & 4u) << 0) | ((z & 7u) << 3);
+}
+__device__ __forceinline__ uint32_t voxel_bit(uint32_t x, uint32_t y) { return (x & 7u) | ((y & 3u) << 3); }
+
 // IsSolid (include/raytracing_functions.cuh:23-26) on the brick layout.
 // Callers pass in-range coordinates (the reference bounds-checks first).
 __device__ __forceinline__ bool is_solid(const World& w, int x, int y, int z) {
-    uint64_t b = brick_of(w, x >> 3, y >> 3, z >> 3);
-    uint32_t local = (uint32_t)(x & 7) | ((uint32_t)(y & 7) << 3) | ((uint32_t)(z & 7) << 6);
-    uint32_t word = w.brick[b * 32 + (local >> 5)];
-    return (word >> (local & 31)) & 1u;
+    uint32_t word = load_dword(w, voxel_word_off(w, (uint32_t)x, (uint32_t)y, (uint32_t)z));
+    return (word >> voxel_bit((uint32_t)x, (uint32_t)y)) & 1u;
 }
 
-// CSDF byte of an in-range coarse cell.
+// CSDF byte of an in-range coarse cell: the dword holding it, then the byte
+// (4x4x4 cells per record, byte = (cx&3) | (cy&3)<<2 | (cz&3)<<4 after 64 B of bits).
 __device__ __forceinline__ uint32_t csdf_at(const World& w, int cx, int cy, int cz) {
-    uint64_t b = brick_of(w, cx >> 2, cy >> 2, cz >> 2);
-    uint32_t local = (uint32_t)(cx & 3) | ((uint32_t)(cy & 3) << 2) | ((uint32_t)(cz & 3) << 4);
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(w.brick) + b * 128 + 64 + local;
-    return *p;
+    uint32_t off = brick_byte(w, (uint32_t)cx >> 2, (uint32_t)cy >> 2, (uint32_t)cz >> 2) | 64u |
+                   (((uint32_t)cy & 3u) << 2) | (((uint32_t)cz & 3u) << 4);
+    return (load_dword(w, off) >> (((uint32_t)cx & 3u) << 3)) & 255u;
 }
 
 // getDistance(float3) (include/raytracing_functions.cuh:35-51): truncating
@@ -235,26 +250,20 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
     uint32_t sphere, dda, check;
 };
 
-// approximateCSDF (src/raytracing_functions.cu:65-83).  Inside the bounds
-// check the coarse index is in range, so no clamp is needed.
-template <bool COUNT>
-__device__ __forceinline__ f3 approximate_csdf(const World& w, f3 pos, f3 dir, StepCount& sc) {
-    for (int it = 0; it < 100; it++) {
-        if (pos.x < 0 || pos.y < 0 || pos.z < 0 || pos.x >= w.fX || pos.y >= w.fY || pos.z >= w.fZ)
-            return V(-100.0f, -100.0f, -100.0f);
-        int cx = (int)(floorf(pos.x) * 0.5f);
-        int cy = (int)(floorf(pos.y) * 0.5f);
-        int cz = (int)(floorf(pos.z) * 0.5f);
-        float d = (float)csdf_at(w, cx, cy, cz);
-        if (COUNT) sc.sphere++;
-        if (d <= 1.0f) return pos;
-        pos = add(pos, scale(dir, d));
-    }
-    return pos;
-}
-
-// trace (src/raytracing_functions.cu:85-202).  dist_h is the already
-// half-rounded start distance (the reference's `half distance`).
+// trace (src/raytracing_functions.cu:85-202) with approximateCSDF (:65-83)
+// inlined.  dist_h is the already half-rounded start distance (the
+// reference's `half distance`).  Same float operation sequence as the
+// reference; the control flow is reshaped for the 64-wide wave:
+//   * bounds tests are one unsigned compare per axis on floor(pos) / ipos
+//     (0 <= p < N  <=>  (unsigned)floor(p) < N for integer N);
+//   * the sphere-march coarse index is floor(p) >> 1 (== (int)(floor(p)*0.5)
+//     for p >= 0, which the bounds test guarantees);
+//   * getDistance(int3)'s trunc-divide + clamp == clamp(ipos >> 1);
+//   * a sphere march that leaves the grid is a miss directly (the reference
+//     returns (-100)^3, whose DDA then fails its bounds test at i = 0);
+//   * the DDA loop has one exit (a status code); the jump and the hit
+//     record are computed after it, so the per-step body is one 4-B gather
+//     plus ~20 VALU instructions.
 template <bool COUNT>
 __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
@@ -269,63 +278,100 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
     const int sx = (dir.x > 0) - (dir.x < 0);
     const int sy = (dir.y > 0) - (dir.y < 0);
     const int sz = (dir.z > 0) - (dir.z < 0);
+    const uint32_t X = (uint32_t)w.X, Y = (uint32_t)w.Y, Z = (uint32_t)w.Z;
+    int ix = 0, iy = 0, iz = 0, mask = -128;
+    float tx = 0.0f, ty = 0.0f, tz = 0.0f;
+    int status = 0;   // 0: gave up (miss), 2: left the grid (miss), 3: hit
     for (int major = 0; major < 5; major++) {
-        cur = approximate_csdf<COUNT>(w, cur, dir, sc);
-        int ix = (int)floorf(cur.x), iy = (int)floorf(cur.y), iz = (int)floorf(cur.z);
-        float tx = ((sx > 0) ? ((float)ix + 1.0f - cur.x) : (cur.x - (float)ix)) * ddx;
-        float ty = ((sy > 0) ? ((float)iy + 1.0f - cur.y) : (cur.y - (float)iy)) * ddy;
-        float tz = ((sz > 0) ? ((float)iz + 1.0f - cur.z) : (cur.z - (float)iz)) * ddz;
-        int mask = -128;
-        bool jumped = false;
-        for (int i = 0; i < 200; i++) {
-            if ((i & 7) == 7) {
-                uint32_t d = get_distance_i(w, ix, iy, iz);
-                if (COUNT) sc.check++;
-                if (d > 2) {
-                    f3 c = V((float)ix + 0.5f, (float)iy + 0.5f, (float)iz + 0.5f);
-                    float t = dot(sub(c, cur), dir);
-                    f3 por = add(cur, scale(dir, t));
-                    cur = add(por, scale(dir, (float)d * 2.0f));
-                    jumped = true;
-                    break;
-                }
-            }
-            if (ix < 0 || iy < 0 || iz < 0 || ix >= w.X || iy >= w.Y || iz >= w.Z) return H;
-            if (COUNT) sc.dda++;
-            if (is_solid(w, ix, iy, iz)) {
-                H.hit = true;
-                if (mask == 0) {
-                    H.normal = V((float)-sx, 0.0f, 0.0f);
-                    H.pos = add(cur, scale(dir, tx - ddx));
-                    H.u = hround(H.pos.y - (float)iy);
-                    H.v = hround(H.pos.z - (float)iz);
-                    if (sx == -1) H.v = hround(1.0f - H.v);
-                } else if (mask == 1) {
-                    H.normal = V(0.0f, (float)-sy, 0.0f);
-                    H.pos = add(cur, scale(dir, ty - ddy));
-                    H.u = hround(H.pos.x - (float)ix);
-                    H.v = hround(H.pos.z - (float)iz);
-                } else if (mask == 2) {
-                    H.normal = V(0.0f, 0.0f, (float)-sz);
-                    H.pos = add(cur, scale(dir, tz - ddz));
-                    H.u = hround(H.pos.x - (float)ix);
-                    H.v = hround(H.pos.y - (float)iy);
-                    if (sz == 1) H.u = hround(1.0f - H.u);
-                } else {
-                    H.undef = true;   // Appendix R2
-                }
-                return H;
-            }
-            if (tx < ty) {
-                if (tx < tz) { tx += ddx; ix += sx; mask = 0; }
-                else         { tz += ddz; iz += sz; mask = 2; }
-            } else {
-                if (ty < tz) { ty += ddy; iy += sy; mask = 1; }
-                else         { tz += ddz; iz += sz; mask = 2; }
-            }
+        // ---- approximateCSDF: sphere-step through the coarse SDF.  The body
+        // is straight-line (clamped, always-valid gather; predicated update)
+        // with a single exit, so a wave pays no divergent-branch bookkeeping.
+        bool oob = false;
+        for (int it = 0; it < 100; it++) {
+            int fx = (int)floorf(cur.x), fy = (int)floorf(cur.y), fz = (int)floorf(cur.z);
+            oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= Y) | ((uint32_t)fz >= Z);
+            uint32_t d = csdf_at(w, min((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u),
+                                 min((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u),
+                                 min((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u));
+            if (COUNT) sc.sphere += !oob;
+            const bool stop = oob | (d <= 1);
+            f3 nxt = add(cur, scale(dir, (float)d));
+            cur.x = stop ? cur.x : nxt.x;
+            cur.y = stop ? cur.y : nxt.y;
+            cur.z = stop ? cur.z : nxt.z;
+            if (stop) break;
         }
-        if (jumped) continue;
-        break;   // 200 DDA steps without hit or jump: miss
+        if (oob) { status = 2; break; }
+        // ---- DDA set-up
+        ix = (int)floorf(cur.x); iy = (int)floorf(cur.y); iz = (int)floorf(cur.z);
+        tx = ((sx > 0) ? ((float)ix + 1.0f - cur.x) : (cur.x - (float)ix)) * ddx;
+        ty = ((sy > 0) ? ((float)iy + 1.0f - cur.y) : (cur.y - (float)iy)) * ddy;
+        tz = ((sz > 0) ? ((float)iz + 1.0f - cur.z) : (cur.z - (float)iz)) * ddz;
+        mask = -128;
+        int st = 0;           // 1: jump, 2: out of bounds, 3: hit
+        uint32_t jd = 0;
+        for (int i = 0; i < 200; i++) {
+            if ((i & 7) == 7) {   // i is wave-uniform: a scalar branch
+                int cx = min(max(ix >> 1, 0), w.SX - 1);
+                int cy = min(max(iy >> 1, 0), w.SY - 1);
+                int cz = min(max(iz >> 1, 0), w.SZ - 1);
+                jd = csdf_at(w, cx, cy, cz);
+                if (COUNT) sc.check++;
+                st = jd > 2 ? 1 : 0;
+            }
+            const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
+            // clamped (always valid) gather; its bit only counts in bounds
+            uint32_t word = load_dword(w, voxel_word_off(w, min((uint32_t)ix, X - 1u), min((uint32_t)iy, Y - 1u),
+                                                         min((uint32_t)iz, Z - 1u)));
+            const bool solid = (word >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
+            if (COUNT) sc.dda += (st == 0) & !oob;
+            st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
+            const bool go = st == 0;
+            const bool cxy = tx < ty, cxz = tx < tz, cyz = ty < tz;
+            const bool selx = go & cxy & cxz;
+            const bool sely = go & !cxy & cyz;
+            const bool selz = go & !(cxy & cxz) & !(!cxy & cyz);
+            tx = selx ? tx + ddx : tx;
+            ty = sely ? ty + ddy : ty;
+            tz = selz ? tz + ddz : tz;
+            ix += selx ? sx : 0;
+            iy += sely ? sy : 0;
+            iz += selz ? sz : 0;
+            mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
+            if (!go) break;
+        }
+        if (st == 1) {        // empty space ahead: jump and restart
+            f3 c = V((float)ix + 0.5f, (float)iy + 0.5f, (float)iz + 0.5f);
+            float t = dot(sub(c, cur), dir);
+            f3 por = add(cur, scale(dir, t));
+            cur = add(por, scale(dir, (float)jd * 2.0f));
+            continue;
+        }
+        status = st;
+        break;                // hit, left the grid, or 200 steps without either
+    }
+    if (status == 3) {
+        H.hit = true;
+        if (mask == 0) {
+            H.normal = V((float)-sx, 0.0f, 0.0f);
+            H.pos = add(cur, scale(dir, tx - ddx));
+            H.u = hround(H.pos.y - (float)iy);
+            H.v = hround(H.pos.z - (float)iz);
+            if (sx == -1) H.v = hround(1.0f - H.v);
+        } else if (mask == 1) {
+            H.normal = V(0.0f, (float)-sy, 0.0f);
+            H.pos = add(cur, scale(dir, ty - ddy));
+            H.u = hround(H.pos.x - (float)ix);
+            H.v = hround(H.pos.z - (float)iz);
+        } else if (mask == 2) {
+            H.normal = V(0.0f, 0.0f, (float)-sz);
+            H.pos = add(cur, scale(dir, tz - ddz));
+            H.u = hround(H.pos.x - (float)ix);
+            H.v = hround(H.pos.y - (float)iy);
+            if (sz == 1) H.u = hround(1.0f - H.u);
+        } else {
+            H.undef = true;   // Appendix R2: pos stays (-500)^3
+        }
     }
     return H;
 }
