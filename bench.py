@@ -35,16 +35,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(st: dict, px: int, halfpx: int, prepass: bool, stage: str) -> int:
-    """4 B per DDA voxel test, 1 B per CSDF read (sphere step or
-    every-8th-step check), 5 B per cone step (1 B CSDF + 4 B GI), 16 B per
-    texture sample; full-res px: 10 B of outputs (+32 B of half-res taps with
-    the pre-pass); half-res px: 8 B of outputs."""
+def algorithmic_bytes(st: dict, px: int, halfpx: int, prepass: bool, stage: str, pp_hits: int = 0) -> int:
+    """Bytes one launch of a stage must move (SURVEY.md s8(d) model, split by
+    wavefront stage).  Traversal: 4 B per DDA voxel test, 1 B per CSDF read
+    (sphere step or every-8th-step check); 5 B per cone step (1 B CSDF + 4 B
+    GI); 16 B per texture sample.  Stage I/O: hit records (16 B position +
+    4 B info), 4 B queue entries, 16 B secondary results, pre-pass outputs
+    (4+4 B), 4 point + 4 bilinear half-res taps (32 B), outputs 10 B/px."""
     b = 4 * st["dda_steps"] + st["sphere_steps"] + st["csdf_checks"]
-    if stage == "render":
-        b += 5 * st["cone_steps"] + 16 * st["tex_samples"] + px * (10 + (32 if prepass else 0))
-    else:
-        b += halfpx * 8
+    b += 5 * st["cone_steps"] + 16 * st["tex_samples"]
+    if stage == "pp_primary":   # 4 B distance per pixel; 16 B hit + 4 B queue per hit, else 4 B shadow
+        b += halfpx * 4 + pp_hits * 20 + (halfpx - pp_hits) * 4
+    elif stage == "pp_shadow":
+        b += st["prepass_shadow"] * (4 + 16 + 4)
+    elif stage == "primary":
+        b += px * (20 + (16 if prepass else 0))
+    elif stage == "shadow":
+        b += st["shadow"] * (4 + 20 + 4)
+    elif stage == "water":
+        b += st["refl"] * (4 + 20 + 16)
+    elif stage == "cones":
+        b += (st["cones"] // 6) * (4 + 20 + 16)
+    elif stage == "shade":
+        b += px * (20 + 10 + (16 if prepass else 0))
+    elif stage == "frame":   # the whole fused frame (per-pixel path)
+        b += px * (10 + (32 if prepass else 0)) + (halfpx * 8 if prepass else 0)
     return int(b)
 
 
@@ -59,6 +74,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
+    ap.add_argument("--flags", type=int, default=None,
+                    help="experiments only: override the config's RV_F_* flags")
     args = ap.parse_args()
 
     import torch
@@ -84,7 +101,7 @@ def main():
 
     cfg = CONFIGS[args.config]
     W, H = cfg.width, cfg.height
-    flags = cfg.flags
+    flags = cfg.flags if args.flags is None else args.flags
     prepass = bool(flags & rv.RV_F_PREPASS)
     atlas = load_atlas()
 
@@ -108,11 +125,14 @@ def main():
     r.stats_reset()
     r.frame(cam, vp, flags=flags | rv.RV_F_STATS)
     st_all = r.stats(-1)
-    st_render = r.stats(0)
-    st_pp = r.stats(1)
+    st_stage = {name: r.stats(k) for k, name in enumerate(rv._lib.STAGES)}
     rays_per_frame = st_all["traces"]
-    b_render = algorithmic_bytes(st_render, W * H, (W // 2) * (H // 2), prepass, "render")
-    b_pp = algorithmic_bytes(st_pp, W * H, (W // 2) * (H // 2), prepass, "prepass") if prepass else 0
+    megakernel = os.environ.get("RV_MEGAKERNEL", "0") == "1"
+    pp_hits = st_stage["pp_shadow"]["prepass_shadow"]
+    stage_bytes = {name: algorithmic_bytes(st_stage[name], W * H, (W // 2) * (H // 2), prepass,
+                                           "frame" if megakernel and name in ("pp_primary", "primary") else name,
+                                           pp_hits)
+                   for name in rv._lib.STAGES if name != "gi"}
 
     # ---------------------------------------------------------------- tiles
     T = args.tile_px
@@ -153,6 +173,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     stage_ms, nframes = r.timing_get()
+    per_stage_ms, _ = r.timing_stages()
     r.timing_enable(0)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -166,25 +187,35 @@ def main():
     fps = args.steps / elapsed
     mrays = rays_per_frame * fps / 1e6
 
-    # dominant kernel: the render stage (k_render / k_render_tiles)
-    render_ms = stage_ms[2] / max(nframes, 1)
-    pp_ms = stage_ms[1] / max(nframes, 1)
-    gi_ms = stage_ms[0] / max(nframes, 1)
-    if world_size == 1:
-        achieved = b_render / (render_ms * 1e-3) / 1e9 if render_ms > 0 else 0.0
-    else:   # per-GPU: this rank's share of the render bytes over its render time
-        achieved = (b_render * len(my_tiles) / ntiles) / (render_ms * 1e-3) / 1e9 if render_ms > 0 else 0.0
+    nf = max(nframes, 1)
+    render_ms = stage_ms[2] / nf
+    pp_ms = stage_ms[1] / nf
+    gi_ms = stage_ms[0] / nf
+    avg_stage_ms = {k: v / nf for k, v in per_stage_ms.items()}
+    # dominant kernel: the frame stage with the largest average launch time
+    dom = max((k for k in avg_stage_ms if k != "gi"), key=lambda k: avg_stage_ms[k])
+    kernel_names = {"pp_primary": "k_prepass" if megakernel else "k_wf_pp_primary",
+                    "pp_shadow": "k_wf_pp_shadow",
+                    "primary": "k_render" if megakernel else "k_wf_primary", "shadow": "k_wf_shadow",
+                    "water": "k_wf_water", "cones": "k_wf_cones", "shade": "k_wf_shade"}
+    dom_ms = avg_stage_ms[dom]
+    dom_bytes = stage_bytes[dom]
+    if world_size > 1:   # per-GPU: this rank's share of the stage's bytes
+        dom_bytes = dom_bytes * len(my_tiles) / ntiles
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):
         try:
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+            tj = json.load(open(tpath))
+            if tj.get("kernel", "").startswith(kernel_names[dom]):
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {"bound": "hbm", "kernel": "k_render", "achieved": round(achieved, 2),
+    roofline = {"bound": "hbm", "kernel": kernel_names[dom], "achieved": round(achieved, 2),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": traffic, "algorithmic_bytes_per_launch": b_render,
-                "avg_launch_ms": round(render_ms, 4)}
+                "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
+                "avg_launch_ms": round(dom_ms, 4)}
 
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
@@ -212,6 +243,8 @@ def main():
                        "parallelism": f"screen-tiles {T}px x{world_size}" if world_size > 1 else "single-gpu"},
             "rays_per_frame": rays_per_frame,
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
+            "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
+            "path": "per-pixel" if megakernel else "wavefront",
             "roofline": roofline,
             "cpu_baseline": cpu,
             "world_build_s": round(world_s, 3),

@@ -18,6 +18,7 @@ RV_FLAGS_REFERENCE = RV_F_PREPASS | RV_F_WATER | RV_F_GI
 RV_IMAGE_COLOR, RV_IMAGE_MOTION, RV_IMAGE_DEPTH, RV_IMAGE_HALF_DIST, RV_IMAGE_HALF_SHADOW = range(5)
 RV_WORLD_BITS, RV_WORLD_CSDF, RV_WORLD_GI = range(3)
 
+STAGES = ["pp_primary", "pp_shadow", "primary", "shadow", "water", "cones", "shade", "gi"]
 STATUS_NAMES = {0: "RV_OK", 1: "RV_ERR_INVALID", 2: "RV_ERR_HIP", 3: "RV_ERR_OOM",
                 4: "RV_ERR_STATE", 5: "RV_ERR_NO_DEVICE"}
 
@@ -88,6 +89,7 @@ SIGNATURES = [
     ("rv_stats_reset", I32, [P]),
     ("rv_timing_enable", I32, [P, I32]),
     ("rv_timing_get", I32, [P, C.POINTER(C.c_double), C.POINTER(I32)]),
+    ("rv_timing_stages", I32, [P, C.POINTER(C.c_double), I32, C.POINTER(I32)]),
     ("rv_sync", I32, [P]),
 ]
 

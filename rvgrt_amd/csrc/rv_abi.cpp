@@ -39,10 +39,16 @@ struct rv_ctx {
     int* tile_ids = nullptr; int tile_cap = 0;
     uint32_t* tilebuf = nullptr; size_t tilebuf_bytes = 0;
     uint32_t* ext_tilebuf = nullptr; size_t ext_tilebuf_bytes = 0;
-    // stage timing (rv_timing_enable): 4 events per frame
+    // stage timing (rv_timing_enable): EV_PER_FRAME events per frame
     int timing_cap = 0, timing_n = 0;
-    bool gi_pending = false;
     std::vector<hipEvent_t> ev;
+    std::vector<char> gi_timed;
+    bool megakernel = false;      // RV_MEGAKERNEL=1: per-pixel k_prepass/k_render path
+    int enq = 1;                  // RV_WF_ENQ: queue append granularity (FrameParams::enq)
+    // wavefront buffers
+    float4* hpos = nullptr; uint32_t* hinfo = nullptr; float4* hsec = nullptr; float4* pphit = nullptr;
+    int* wq[NQUEUE] = {nullptr, nullptr, nullptr, nullptr};
+    unsigned* qcount = nullptr;
     uint32_t gi_frame = 0;
     uint64_t gi_offset = 0;
     bool world_ready = false;
@@ -69,6 +75,10 @@ rv_status fail(rv_ctx* c, rv_status s, const std::string& msg) {
 #define LAUNCH_CHECK(ctx) HIP_TRY(ctx, hipGetLastError())
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// per frame: [0, NSTAGE-1) start of each frame stage, [NSTAGE-1] end of the
+// frame, [NSTAGE] / [NSTAGE+1] start / end of the GI update before it
+constexpr int EV_PER_FRAME = NSTAGE + 2;
 
 uint64_t n_gi(const rv_ctx* c) { return (uint64_t)c->w.GX * c->w.GY * c->w.GZ; }
 uint64_t n_csdf(const rv_ctx* c) { return (uint64_t)c->w.SX * c->w.SY * c->w.SZ; }
@@ -105,6 +115,8 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (cfg->log2_x < 4 || cfg->log2_y < 4 || cfg->log2_z < 4 || cfg->log2_x > 13 || cfg->log2_y > 13 ||
         cfg->log2_z > 13)
         return RV_ERR_INVALID;
+    // brick records must stay below 4 GiB (32-bit gather offsets): <= 2^34 voxels
+    if (cfg->log2_x + cfg->log2_y + cfg->log2_z > 34) return RV_ERR_INVALID;
     if (cfg->width < 2 || cfg->height < 2 || (cfg->width & 1) || (cfg->height & 1)) return RV_ERR_INVALID;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return RV_ERR_NO_DEVICE;
@@ -171,9 +183,21 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
     if (hipMalloc(&c->queue, 16) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "queue");
     hipMemset(c->queue, 0, 16);
-    if (hipMalloc(&c->counters, 2 * NCNT * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc(&c->counters, NSTAGE * NCNT * sizeof(unsigned long long)) != hipSuccess)
         return cleanup_fail(RV_ERR_OOM, "counters");
-    hipMemset(c->counters, 0, 2 * NCNT * sizeof(unsigned long long));
+    hipMemset(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long));
+    if (const char* e = getenv("RV_MEGAKERNEL")) c->megakernel = atoi(e) != 0;
+    if (const char* e = getenv("RV_WF_ENQ")) c->enq = atoi(e);
+    {   // wavefront stage buffers
+        size_t npx = (size_t)W * H, nhalf = (size_t)(W / 2) * (H / 2);
+        bool ok = hipMalloc(&c->hpos, npx * 16) == hipSuccess && hipMalloc(&c->hinfo, npx * 4) == hipSuccess &&
+                  hipMalloc(&c->hsec, npx * 16) == hipSuccess && hipMalloc(&c->pphit, nhalf * 16) == hipSuccess &&
+                  hipMalloc(&c->qcount, 64) == hipSuccess;
+        // Q_PP holds half-res pixels, duplicated at most 4x by tile halos
+        for (int q = 0; q < NQUEUE && ok; q++) ok = hipMalloc(&c->wq[q], npx * 4) == hipSuccess;
+        if (!ok) return cleanup_fail(RV_ERR_OOM, "wavefront buffers");
+        hipMemset(c->qcount, 0, 64);
+    }
     if (hipDeviceSynchronize() != hipSuccess) return cleanup_fail(RV_ERR_HIP, "init sync");
     *out = c;
     return RV_OK;
@@ -187,6 +211,8 @@ void rv_destroy(rv_ctx* c) {
     hipFree(c->own_color); hipFree(c->own_mv); hipFree(c->own_depth);
     hipFree(c->hdist); hipFree(c->hshadow); hipFree(c->counters);
     hipFree(c->tile_ids); hipFree(c->tilebuf); hipFree(c->queue);
+    hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
+    for (int q = 0; q < NQUEUE; q++) hipFree(c->wq[q]);
     for (hipEvent_t e : c->ev) hipEventDestroy(e);
     delete c;
 }
@@ -218,7 +244,7 @@ rv_status rv_csdf_build(rv_ctx* c) {
 
 rv_status rv_gi_init(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
-    launch_gi_init(c->stream, c->gi, current_world(c), sun_dir(), c->counters);
+    launch_gi_init(c->stream, c->gi, current_world(c), sun_dir(), c->counters + ST_GI * NCNT);
     LAUNCH_CHECK(c);
     c->gi_frame = 0;
     c->gi_offset = 0;
@@ -304,7 +330,8 @@ rv_status rv_gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t count
     if (first >= n) return RV_OK;
     if (first + count > n) count = n - first;
     if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
-    launch_gi_update(c->stream, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count, c->counters);
+    launch_gi_update(c->stream, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count,
+                     c->counters + ST_GI * NCNT);
     LAUNCH_CHECK(c);
     if (count == n) {
         std::swap(c->gi, c->gi_tmp);   // full sweep: flip the double buffer
@@ -318,12 +345,14 @@ rv_status rv_gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t count
 rv_status rv_update_gi_data(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     uint64_t rays = c->cfg.gi_rays_per_frame, n = n_gi(c);
-    if (c->timing_n < c->timing_cap) {
-        HIP_TRY(c, hipEventRecord(c->ev[4 * c->timing_n + 0], c->stream));
-        c->gi_pending = true;
-    }
+    const bool timed = c->timing_n < c->timing_cap;
+    if (timed) HIP_TRY(c, hipEventRecord(c->ev[EV_PER_FRAME * c->timing_n + NSTAGE], c->stream));
     rv_status s = rv_gi_update(c, c->gi_frame, c->gi_offset, rays);
     if (s != RV_OK) return s;
+    if (timed) {
+        HIP_TRY(c, hipEventRecord(c->ev[EV_PER_FRAME * c->timing_n + NSTAGE + 1], c->stream));
+        c->gi_timed[c->timing_n] = 1;
+    }
     c->gi_frame++;
     if (c->gi_offset + rays >= n) c->gi_offset = 0;   // src/CoarseArray.cu:392-394
     else c->gi_offset += rays;
@@ -352,33 +381,55 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
     f.counters = c->counters;
     f.sched = c->sched;
     f.queue = c->queue;
+    f.hpos = c->hpos; f.hinfo = c->hinfo; f.hsec = c->hsec; f.pphit = c->pphit;
+    for (int q = 0; q < NQUEUE; q++) f.queue_wf[q] = c->wq[q];
+    f.qcount = c->qcount;
+    f.enq = c->enq;
     return f;
 }
 
-// Enqueue pre-pass + render, recording stage events when timing is on.
+// Enqueue the frame's stages, recording a start event per stage when timing
+// is on.  Each stage counts into its own counter block (rv_stats_stage).
 static rv_status run_stages(rv_ctx* c, const FrameParams& f, bool tiles) {
-    bool timed = c->timing_n < c->timing_cap;
-    hipEvent_t* e = timed ? &c->ev[4 * c->timing_n] : nullptr;
+    const bool timed = c->timing_n < c->timing_cap;
+    hipEvent_t* e = timed ? &c->ev[(size_t)EV_PER_FRAME * c->timing_n] : nullptr;
     World w = current_world(c);
-    if (c->sched == SCHED_QUEUE) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 16, c->stream));
-    if (timed) {
-        if (!c->gi_pending) HIP_TRY(c, hipEventRecord(e[0], c->stream));
-        HIP_TRY(c, hipEventRecord(e[1], c->stream));
-    }
-    if (f.flags & RV_F_PREPASS) {
-        FrameParams fp = f;
-        fp.counters = c->counters + NCNT;   // pre-pass counters kept apart (rv_stats_stage)
-        if (tiles) launch_prepass_tiles(c->stream, w, fp); else launch_prepass(c->stream, w, fp);
+    auto mark = [&](int k) -> hipError_t { return timed ? hipEventRecord(e[k], c->stream) : hipSuccess; };
+    auto stage = [&](int k) { FrameParams g = f; g.counters = c->counters + (size_t)k * NCNT; return g; };
+    const bool pre = (f.flags & RV_F_PREPASS) != 0;
+    if (c->megakernel) {
+        if (c->sched == SCHED_QUEUE) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 16, c->stream));
+        HIP_TRY(c, mark(ST_PP_PRIMARY));
+        if (pre) {
+            if (tiles) launch_prepass_tiles(c->stream, w, stage(ST_PP_PRIMARY));
+            else launch_prepass(c->stream, w, stage(ST_PP_PRIMARY));
+            LAUNCH_CHECK(c);
+        }
+        for (int k = ST_PP_SHADOW; k <= ST_PRIMARY; k++) HIP_TRY(c, mark(k));
+        if (tiles) launch_render_tiles(c->stream, w, stage(ST_PRIMARY)); else launch_render(c->stream, w, stage(ST_PRIMARY));
         LAUNCH_CHECK(c);
+        for (int k = ST_SHADOW; k <= ST_SHADE + 1; k++) HIP_TRY(c, mark(k));
+    } else {
+        HIP_TRY(c, hipMemsetAsync(c->qcount, 0, 64, c->stream));
+        HIP_TRY(c, mark(ST_PP_PRIMARY));
+        if (pre) { launch_wf_pp_primary(c->stream, w, stage(ST_PP_PRIMARY), tiles); LAUNCH_CHECK(c); }
+        HIP_TRY(c, mark(ST_PP_SHADOW));
+        if (pre) { launch_wf_pp_shadow(c->stream, w, stage(ST_PP_SHADOW)); LAUNCH_CHECK(c); }
+        HIP_TRY(c, mark(ST_PRIMARY));
+        launch_wf_primary(c->stream, w, stage(ST_PRIMARY), tiles);
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, mark(ST_SHADOW));
+        if (!pre && (f.flags & RV_F_SHADOW)) { launch_wf_shadow(c->stream, w, stage(ST_SHADOW)); LAUNCH_CHECK(c); }
+        HIP_TRY(c, mark(ST_WATER));
+        if (f.flags & RV_F_WATER) { launch_wf_water(c->stream, w, stage(ST_WATER)); LAUNCH_CHECK(c); }
+        HIP_TRY(c, mark(ST_CONES));
+        if (f.flags & RV_F_GI) { launch_wf_cones(c->stream, w, stage(ST_CONES)); LAUNCH_CHECK(c); }
+        HIP_TRY(c, mark(ST_SHADE));
+        launch_wf_shade(c->stream, w, stage(ST_SHADE), tiles);
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, mark(ST_SHADE + 1));
     }
-    if (timed) HIP_TRY(c, hipEventRecord(e[2], c->stream));
-    if (tiles) launch_render_tiles(c->stream, w, f); else launch_render(c->stream, w, f);
-    LAUNCH_CHECK(c);
-    if (timed) {
-        HIP_TRY(c, hipEventRecord(e[3], c->stream));
-        c->timing_n++;
-        c->gi_pending = false;
-    }
+    if (timed) c->timing_n++;
     return RV_OK;
 }
 
@@ -460,25 +511,43 @@ rv_status rv_timing_enable(rv_ctx* c, int32_t max_frames) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (hipEvent_t e : c->ev) hipEventDestroy(e);
     c->ev.clear();
-    c->timing_cap = 0; c->timing_n = 0; c->gi_pending = false;
-    c->ev.resize((size_t)max_frames * 4);
+    c->timing_cap = 0; c->timing_n = 0;
+    c->ev.resize((size_t)max_frames * EV_PER_FRAME);
+    c->gi_timed.assign((size_t)max_frames, 0);
     for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
     c->timing_cap = max_frames;
     return RV_OK;
 }
 
-rv_status rv_timing_get(rv_ctx* c, double ms[3], int32_t* frames) {
-    if (!c || !ms) return RV_ERR_INVALID;
+rv_status rv_timing_stages(rv_ctx* c, double* ms, int32_t n, int32_t* frames) {
+    if (!c || !ms || n < 0) return RV_ERR_INVALID;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    ms[0] = ms[1] = ms[2] = 0.0;
+    for (int k = 0; k < n; k++) ms[k] = 0.0;
     for (int i = 0; i < c->timing_n; i++) {
-        for (int k = 0; k < 3; k++) {
+        hipEvent_t* e = &c->ev[(size_t)EV_PER_FRAME * i];
+        for (int k = 0; k < NSTAGE - 1 && k < n; k++) {
             float t = 0.0f;
-            HIP_TRY(c, hipEventElapsedTime(&t, c->ev[4 * i + k], c->ev[4 * i + k + 1]));
+            HIP_TRY(c, hipEventElapsedTime(&t, e[k], e[k + 1]));
             ms[k] += t;
+        }
+        if (c->gi_timed[i] && ST_GI < n) {
+            float t = 0.0f;
+            HIP_TRY(c, hipEventElapsedTime(&t, e[NSTAGE], e[NSTAGE + 1]));
+            ms[ST_GI] += t;
         }
     }
     if (frames) *frames = c->timing_n;
+    return RV_OK;
+}
+
+rv_status rv_timing_get(rv_ctx* c, double ms[3], int32_t* frames) {
+    if (!c || !ms) return RV_ERR_INVALID;
+    double st[NSTAGE];
+    rv_status s = rv_timing_stages(c, st, NSTAGE, frames);
+    if (s != RV_OK) return s;
+    ms[0] = st[ST_GI];
+    ms[1] = st[ST_PP_PRIMARY] + st[ST_PP_SHADOW];
+    ms[2] = st[ST_PRIMARY] + st[ST_SHADOW] + st[ST_WATER] + st[ST_CONES] + st[ST_SHADE];
     return RV_OK;
 }
 
@@ -640,16 +709,17 @@ rv_status rv_camera_from_pose(float px, float py, float pz, float yaw, float pit
     return RV_OK;
 }
 
-// counters: block 0 = everything but the pre-pass, block 1 = pre-pass
+// counters: one block of NCNT per frame stage (ST_*), -1 = their sum
 rv_status rv_stats_stage(rv_ctx* c, int32_t stage, rv_stats* out) {
-    if (!c || !out || stage < -1 || stage > 1) return RV_ERR_INVALID;
-    unsigned long long h[2 * NCNT];
-    HIP_TRY(c, hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    if (!c || !out || stage < -1 || stage >= NSTAGE) return RV_ERR_INVALID;
+    std::vector<unsigned long long> h((size_t)NSTAGE * NCNT);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->counters, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     static_assert(sizeof(rv_stats) == NCNT * 8, "rv_stats layout");
-    unsigned long long r[NCNT];
-    for (int k = 0; k < NCNT; k++)
-        r[k] = stage < 0 ? h[k] + h[NCNT + k] : h[stage * NCNT + k];
+    unsigned long long r[NCNT] = {};
+    for (int s = 0; s < NSTAGE; s++)
+        if (stage < 0 || s == stage)
+            for (int k = 0; k < NCNT; k++) r[k] += h[(size_t)s * NCNT + k];
     std::memcpy(out, r, sizeof(r));
     return RV_OK;
 }
@@ -658,7 +728,7 @@ rv_status rv_stats_get(rv_ctx* c, rv_stats* out) { return rv_stats_stage(c, -1, 
 
 rv_status rv_stats_reset(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
-    HIP_TRY(c, hipMemsetAsync(c->counters, 0, 2 * NCNT * sizeof(unsigned long long), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long), c->stream));
     return RV_OK;
 }
 

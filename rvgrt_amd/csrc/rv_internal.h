@@ -19,6 +19,15 @@ enum {
 // workgroup -> pixel-block scheduling of the frame kernels (see rv_kernels.hip)
 enum { SCHED_IDENTITY = 0, SCHED_BAND = 1, SCHED_CHUNK = 2, SCHED_QUEUE = 3 };
 
+// Frame stages: one counter block (RV_F_STATS) and one timing slot each.
+// Wavefront path: PP_PRIMARY, PP_SHADOW, PRIMARY, SHADOW, WATER, CONES, SHADE;
+// per-pixel (megakernel) path: PP_PRIMARY = k_prepass, PRIMARY = k_render.
+enum { ST_PP_PRIMARY = 0, ST_PP_SHADOW, ST_PRIMARY, ST_SHADOW, ST_WATER, ST_CONES, ST_SHADE, ST_GI, NSTAGE };
+// Work queues of the wavefront path (pixel indices, ballot-compacted).
+enum { Q_PP = 0, Q_SHADOW, Q_WATER, Q_CONE, NQUEUE };
+// hinfo bits of a primary hit record
+enum : uint32_t { HI_HIT = 1u, HI_UNDEF = 2u, HI_WATER = 4u, HI_SHADOWED = 8u, HI_NSHIFT = 4 };
+
 struct FrameParams {
     int sched;
     unsigned* queue;   // [0] pre-pass, [1] render work counters (SCHED_QUEUE)
@@ -33,6 +42,14 @@ struct FrameParams {
     unsigned long long* counters;
     const int* tiles; int ntiles; int tile_px; int tiles_x;
     uint32_t* tilebuf;
+    // wavefront buffers (full res unless noted)
+    float4* hpos;           // primary hit position xyz, w = uv half bits (u | v << 16)
+    uint32_t* hinfo;        // HI_* flags | normal code << HI_NSHIFT
+    float4* hsec;           // water colour (pre-fog) or summed cone light
+    float4* pphit;          // half res: pre-pass hit position, w = normal code bits
+    int* queue_wf[NQUEUE];
+    unsigned* qcount;       // NQUEUE counters, zeroed before every frame
+    int enq;                // queue append: 0 one atomic per wave, 1 per workgroup
 };
 
 struct RvHitDev {   // == rv_hit
@@ -54,6 +71,15 @@ void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
 void launch_prepass_tiles(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render_tiles(hipStream_t s, const World& w, const FrameParams& f);
+// wavefront stages (rv_wavefront.hip); `counters` of f must point at the
+// stage's own counter block
+void launch_wf_pp_primary(hipStream_t s, const World& w, const FrameParams& f, bool tiles);
+void launch_wf_pp_shadow(hipStream_t s, const World& w, const FrameParams& f);
+void launch_wf_primary(hipStream_t s, const World& w, const FrameParams& f, bool tiles);
+void launch_wf_shadow(hipStream_t s, const World& w, const FrameParams& f);
+void launch_wf_water(hipStream_t s, const World& w, const FrameParams& f);
+void launch_wf_cones(hipStream_t s, const World& w, const FrameParams& f);
+void launch_wf_shade(hipStream_t s, const World& w, const FrameParams& f, bool tiles);
 void launch_untile(hipStream_t s, const uint32_t* tiles, const int* ids, int ntiles, int tile_px, int tiles_x,
                    int W, int H, uint32_t* color, size_t pitch);
 void launch_trace_rays(hipStream_t s, const World& w, const float* org, const float* dir, const float* dist,

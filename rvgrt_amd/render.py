@@ -205,7 +205,7 @@ class StateRender:
         return np.frombuffer(bytes(out), dt, count=n).copy()
 
     def stats(self, stage=-1) -> dict:
-        """Counters (RV_F_STATS frames): stage -1 all, 0 non-pre-pass, 1 pre-pass."""
+        """Counters (RV_F_STATS frames) of one RV_STAGE_* (-1 = all stages)."""
         s = rv_stats()
         self._check(self._L.rv_stats_stage(self._h, int(stage), C.byref(s)), "rv_stats_stage")
         return s.as_dict()
@@ -219,6 +219,14 @@ class StateRender:
         n = C.c_int32()
         self._check(self._L.rv_timing_get(self._h, ms, C.byref(n)), "rv_timing_get")
         return list(ms), n.value
+
+    def timing_stages(self):
+        """({stage name: summed ms}, frames) for the RV_STAGE_* slots."""
+        n = len(_lib.STAGES)
+        ms = (C.c_double * n)()
+        k = C.c_int32()
+        self._check(self._L.rv_timing_stages(self._h, ms, n, C.byref(k)), "rv_timing_stages")
+        return dict(zip(_lib.STAGES, list(ms))), k.value
 
     def stats_reset(self):
         self._check(self._L.rv_stats_reset(self._h), "rv_stats_reset")

@@ -206,3 +206,27 @@ def test_golden_fixtures(rv, atlas):
             assert np.array_equal(h["u"], t["u"]) and np.array_equal(h["v"], t["v"])
             assert np.array_equal(h["dda_steps"], t["n_dda"])
         r.close()
+
+
+@pytest.mark.parametrize("flags", [0, 8, 7])
+def test_wavefront_equals_per_pixel_path(rv, atlas, flags, monkeypatch):
+    """The wavefront stages and the per-pixel (megakernel) path are two
+    schedules of the same arithmetic: images and counters are identical."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H = 7, 320, 192
+    out = {}
+    for mk in ("0", "1"):
+        monkeypatch.setenv("RV_MEGAKERNEL", mk)
+        r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+        for pose in ("P0", "P1"):
+            cam, vp = rv.camera_from_pose(*TEST_POSES_128[pose], W, H)
+            r.stats_reset()
+            r.frame(cam, vp, flags=flags | rv.RV_F_STATS)
+            out[(mk, pose)] = (r.readback(rv.RV_IMAGE_COLOR).copy(), r.readback(rv.RV_IMAGE_MOTION).copy(),
+                               r.readback(rv.RV_IMAGE_DEPTH).copy(), r.stats())
+        r.close()
+    for pose in ("P0", "P1"):
+        a, b = out[("0", pose)], out[("1", pose)]
+        for k in range(3):
+            assert np.array_equal(a[k], b[k]), (pose, k)
+        assert a[3] == b[3]
