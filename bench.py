@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
+    ap.add_argument("--path", default="fused", choices=["fused", "wavefront"],
+                    help="frame path: per-pixel megakernels (default) or wavefront stage kernels")
+    ap.add_argument("--gi-async", type=int, default=1, help="overlap the GI update with the previous render")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
     args = ap.parse_args()
@@ -109,6 +112,8 @@ def main():
     r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=flags, atlas=atlas, device=local_rank)
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream.cuda_stream)
+    r.set_frame_path(args.path)
+    r.set_gi_async(args.gi_async)
     t0 = time.perf_counter()
     r.world_build()
     for s in range(max(cfg.gi_sweeps, 0)):
@@ -127,7 +132,7 @@ def main():
     st_all = r.stats(-1)
     st_stage = {name: r.stats(k) for k, name in enumerate(rv._lib.STAGES)}
     rays_per_frame = st_all["traces"]
-    megakernel = os.environ.get("RV_MEGAKERNEL", "0") == "1"
+    megakernel = args.path == "fused"
     pp_hits = st_stage["pp_shadow"]["prepass_shadow"]
     stage_bytes = {name: algorithmic_bytes(st_stage[name], W * H, (W // 2) * (H // 2), prepass,
                                            "frame" if megakernel and name in ("pp_primary", "primary") else name,
@@ -244,7 +249,7 @@ def main():
             "rays_per_frame": rays_per_frame,
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
-            "path": "per-pixel" if megakernel else "wavefront",
+            "path": args.path, "gi_async": bool(args.gi_async),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "world_build_s": round(world_s, 3),

@@ -17,6 +17,7 @@ RV_F_PREPASS, RV_F_WATER, RV_F_GI, RV_F_SHADOW, RV_F_STATS = 1, 2, 4, 8, 16
 RV_FLAGS_REFERENCE = RV_F_PREPASS | RV_F_WATER | RV_F_GI
 RV_IMAGE_COLOR, RV_IMAGE_MOTION, RV_IMAGE_DEPTH, RV_IMAGE_HALF_DIST, RV_IMAGE_HALF_SHADOW = range(5)
 RV_WORLD_BITS, RV_WORLD_CSDF, RV_WORLD_GI = range(3)
+RV_PATH_FUSED, RV_PATH_WAVEFRONT = 0, 1
 
 STAGES = ["pp_primary", "pp_shadow", "primary", "shadow", "water", "cones", "shade", "gi"]
 STATUS_NAMES = {0: "RV_OK", 1: "RV_ERR_INVALID", 2: "RV_ERR_HIP", 3: "RV_ERR_OOM",
@@ -66,6 +67,8 @@ SIGNATURES = [
     ("rv_destroy", None, [P]),
     ("rv_last_error", C.c_char_p, [P]),
     ("rv_set_stream", I32, [P, P]),
+    ("rv_set_frame_path", I32, [P, I32]),
+    ("rv_set_gi_async", I32, [P, I32]),
     ("rv_world_build", I32, [P]),
     ("rv_world_import", I32, [P, I32, P, SZ]),
     ("rv_world_export", I32, [P, I32, P, SZ]),

@@ -43,11 +43,17 @@ struct rv_ctx {
     int timing_cap = 0, timing_n = 0;
     std::vector<hipEvent_t> ev;
     std::vector<char> gi_timed;
-    bool megakernel = false;      // RV_MEGAKERNEL=1: per-pixel k_prepass/k_render path
+    bool megakernel = true;       // RV_PATH_FUSED (k_prepass/k_render); false: wavefront stages
+    // asynchronous GI update (rv_set_gi_async): kernel on gi_stream, copy-back on stream
+    bool gi_async = true;
+    hipStream_t gi_stream = nullptr;
+    hipEvent_t ev_world = nullptr;    // recorded on `stream` after the last world/GI write
+    hipEvent_t ev_gi_done = nullptr;  // recorded on gi_stream after a GI kernel
     int enq = 1;                  // RV_WF_ENQ: queue append granularity (FrameParams::enq)
     // wavefront buffers
     float4* hpos = nullptr; uint32_t* hinfo = nullptr; float4* hsec = nullptr; float4* pphit = nullptr;
     int* wq[NQUEUE] = {nullptr, nullptr, nullptr, nullptr};
+    size_t wq_cap[NQUEUE] = {0, 0, 0, 0};   // items allocated per queue (all sub-queues)
     unsigned* qcount = nullptr;
     uint32_t gi_frame = 0;
     uint64_t gi_offset = 0;
@@ -192,12 +198,14 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
         size_t npx = (size_t)W * H, nhalf = (size_t)(W / 2) * (H / 2);
         bool ok = hipMalloc(&c->hpos, npx * 16) == hipSuccess && hipMalloc(&c->hinfo, npx * 4) == hipSuccess &&
                   hipMalloc(&c->hsec, npx * 16) == hipSuccess && hipMalloc(&c->pphit, nhalf * 16) == hipSuccess &&
-                  hipMalloc(&c->qcount, 64) == hipSuccess;
-        // Q_PP holds half-res pixels, duplicated at most 4x by tile halos
-        for (int q = 0; q < NQUEUE && ok; q++) ok = hipMalloc(&c->wq[q], npx * 4) == hipSuccess;
+                  hipMalloc(&c->qcount, QCOUNT_BYTES) == hipSuccess;
         if (!ok) return cleanup_fail(RV_ERR_OOM, "wavefront buffers");
-        hipMemset(c->qcount, 0, 64);
+        hipMemset(c->qcount, 0, QCOUNT_BYTES);   // queues themselves: sized per frame by ensure_queues
     }
+    if (hipEventCreateWithFlags(&c->ev_world, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gi_done, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->gi_stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup_fail(RV_ERR_HIP, "gi stream/events");
     if (hipDeviceSynchronize() != hipSuccess) return cleanup_fail(RV_ERR_HIP, "init sync");
     *out = c;
     return RV_OK;
@@ -214,12 +222,34 @@ void rv_destroy(rv_ctx* c) {
     hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
     for (int q = 0; q < NQUEUE; q++) hipFree(c->wq[q]);
     for (hipEvent_t e : c->ev) hipEventDestroy(e);
+    if (c->gi_stream) { hipStreamSynchronize(c->gi_stream); hipStreamDestroy(c->gi_stream); }
+    if (c->ev_world) hipEventDestroy(c->ev_world);
+    if (c->ev_gi_done) hipEventDestroy(c->ev_gi_done);
     delete c;
 }
 
 rv_status rv_set_stream(rv_ctx* c, void* s) {
     if (!c) return RV_ERR_INVALID;
     c->stream = (hipStream_t)s;
+    return RV_OK;
+}
+
+// Everything that writes the world or the GI grid runs on `stream`; the GI
+// side stream waits on this mark before it reads them.
+static rv_status mark_world(rv_ctx* c) {
+    HIP_TRY(c, hipEventRecord(c->ev_world, c->stream));
+    return RV_OK;
+}
+
+rv_status rv_set_frame_path(rv_ctx* c, int32_t path) {
+    if (!c || (path != RV_PATH_FUSED && path != RV_PATH_WAVEFRONT)) return RV_ERR_INVALID;
+    c->megakernel = path == RV_PATH_FUSED;
+    return RV_OK;
+}
+
+rv_status rv_set_gi_async(rv_ctx* c, int32_t on) {
+    if (!c) return RV_ERR_INVALID;
+    c->gi_async = on != 0;
     return RV_OK;
 }
 
@@ -239,7 +269,7 @@ rv_status rv_csdf_build(rv_ctx* c) {
     LAUNCH_CHECK(c);
     HIP_TRY(c, hipFreeAsync(t0, c->stream));
     HIP_TRY(c, hipFreeAsync(t1, c->stream));
-    return RV_OK;
+    return mark_world(c);
 }
 
 rv_status rv_gi_init(rv_ctx* c) {
@@ -248,7 +278,7 @@ rv_status rv_gi_init(rv_ctx* c) {
     LAUNCH_CHECK(c);
     c->gi_frame = 0;
     c->gi_offset = 0;
-    return RV_OK;
+    return mark_world(c);
 }
 
 rv_status rv_world_build(rv_ctx* c) {
@@ -291,7 +321,7 @@ rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t byte
         return fail(c, RV_ERR_INVALID, "bad world kind");
     }
     c->world_ready = true;
-    return RV_OK;
+    return mark_world(c);
 }
 
 rv_status rv_world_export(rv_ctx* c, int32_t kind, void* host, size_t bytes) {
@@ -324,35 +354,52 @@ rv_status rv_world_export(rv_ctx* c, int32_t kind, void* host, size_t bytes) {
     return RV_OK;
 }
 
-rv_status rv_gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t count) {
-    if (!c) return RV_ERR_INVALID;
+// One GI update over [first, first+count).  Serial: kernel + copy-back on
+// `stream`.  Async (partial ranges only): the kernel runs on gi_stream after
+// the last world/GI write and overlaps whatever `stream` has queued since
+// (the previous frame's render, which reads `gi` only); `stream` waits for
+// it before copying the range back, so every later reader sees the update.
+static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t count, bool async,
+                           hipEvent_t t0, hipEvent_t t1) {
     uint64_t n = n_gi(c);
     if (first >= n) return RV_OK;
     if (first + count > n) count = n - first;
     if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
-    launch_gi_update(c->stream, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count,
+    if (count == n) async = false;   // full sweep flips the double buffer instead
+    hipStream_t ks = async ? c->gi_stream : c->stream;
+    if (async) HIP_TRY(c, hipStreamWaitEvent(ks, c->ev_world, 0));
+    if (t0) HIP_TRY(c, hipEventRecord(t0, ks));
+    launch_gi_update(ks, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count,
                      c->counters + ST_GI * NCNT);
     LAUNCH_CHECK(c);
+    if (t1) HIP_TRY(c, hipEventRecord(t1, ks));
+    if (async) {
+        HIP_TRY(c, hipEventRecord(c->ev_gi_done, ks));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_gi_done, 0));
+    }
     if (count == n) {
         std::swap(c->gi, c->gi_tmp);   // full sweep: flip the double buffer
     } else {
         HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice,
                                   c->stream));
     }
-    return RV_OK;
+    return mark_world(c);
+}
+
+rv_status rv_gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t count) {
+    if (!c) return RV_ERR_INVALID;
+    return gi_update(c, frame, first, count, false, nullptr, nullptr);
 }
 
 rv_status rv_update_gi_data(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     uint64_t rays = c->cfg.gi_rays_per_frame, n = n_gi(c);
     const bool timed = c->timing_n < c->timing_cap;
-    if (timed) HIP_TRY(c, hipEventRecord(c->ev[EV_PER_FRAME * c->timing_n + NSTAGE], c->stream));
-    rv_status s = rv_gi_update(c, c->gi_frame, c->gi_offset, rays);
+    hipEvent_t* e = timed ? &c->ev[(size_t)EV_PER_FRAME * c->timing_n] : nullptr;
+    rv_status s = gi_update(c, c->gi_frame, c->gi_offset, rays, c->gi_async, timed ? e[NSTAGE] : nullptr,
+                            timed ? e[NSTAGE + 1] : nullptr);
     if (s != RV_OK) return s;
-    if (timed) {
-        HIP_TRY(c, hipEventRecord(c->ev[EV_PER_FRAME * c->timing_n + NSTAGE + 1], c->stream));
-        c->gi_timed[c->timing_n] = 1;
-    }
+    if (timed) c->gi_timed[c->timing_n] = 1;
     c->gi_frame++;
     if (c->gi_offset + rays >= n) c->gi_offset = 0;   // src/CoarseArray.cu:392-394
     else c->gi_offset += rays;
@@ -390,7 +437,31 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
 
 // Enqueue the frame's stages, recording a start event per stage when timing
 // is on.  Each stage counts into its own counter block (rv_stats_stage).
-static rv_status run_stages(rv_ctx* c, const FrameParams& f, bool tiles) {
+// Per-XCD sub-queue capacities of this frame's producer grids (FrameParams
+// ::qcap); grows the queue buffers when a tile list needs more room.
+static rv_status ensure_queues(rv_ctx* c, FrameParams& f, bool tiles) {
+    for (int q = 0; q < NQUEUE; q++) {
+        uint32_t blocks = wf_producer_blocks(f, q, tiles);
+        f.qcap[q] = (blocks + NXCD - 1) / NXCD * 256;
+        size_t need = (size_t)NXCD * f.qcap[q];
+        if (need > c->wq_cap[q]) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            hipFree(c->wq[q]);
+            c->wq[q] = nullptr;
+            c->wq_cap[q] = 0;
+            if (hipMalloc(&c->wq[q], need * 4) != hipSuccess) return fail(c, RV_ERR_OOM, "wavefront queues");
+            c->wq_cap[q] = need;
+        }
+        f.queue_wf[q] = c->wq[q];
+    }
+    return RV_OK;
+}
+
+static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
+    if (!c->megakernel) {
+        rv_status st = ensure_queues(c, f, tiles);
+        if (st != RV_OK) return st;
+    }
     const bool timed = c->timing_n < c->timing_cap;
     hipEvent_t* e = timed ? &c->ev[(size_t)EV_PER_FRAME * c->timing_n] : nullptr;
     World w = current_world(c);
@@ -410,7 +481,7 @@ static rv_status run_stages(rv_ctx* c, const FrameParams& f, bool tiles) {
         LAUNCH_CHECK(c);
         for (int k = ST_SHADOW; k <= ST_SHADE + 1; k++) HIP_TRY(c, mark(k));
     } else {
-        HIP_TRY(c, hipMemsetAsync(c->qcount, 0, 64, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->qcount, 0, QCOUNT_BYTES, c->stream));
         HIP_TRY(c, mark(ST_PP_PRIMARY));
         if (pre) { launch_wf_pp_primary(c->stream, w, stage(ST_PP_PRIMARY), tiles); LAUNCH_CHECK(c); }
         HIP_TRY(c, mark(ST_PP_SHADOW));

@@ -25,6 +25,14 @@ enum { SCHED_IDENTITY = 0, SCHED_BAND = 1, SCHED_CHUNK = 2, SCHED_QUEUE = 3 };
 enum { ST_PP_PRIMARY = 0, ST_PP_SHADOW, ST_PRIMARY, ST_SHADOW, ST_WATER, ST_CONES, ST_SHADE, ST_GI, NSTAGE };
 // Work queues of the wavefront path (pixel indices, ballot-compacted).
 enum { Q_PP = 0, Q_SHADOW, Q_WATER, Q_CONE, NQUEUE };
+// Every queue is split into one sub-queue per XCD: a producer workgroup
+// appends to the sub-queue of the XCD it runs on (linear workgroup id mod 8,
+// the hardware's round-robin dispatch) and the consumer grid hands sub-queue
+// x back to workgroups on XCD x, so secondary rays meet the L2 that already
+// holds their primary rays' bricks.  Counters sit 128 B apart.
+enum { NXCD = 8, QC_STRIDE = 32 };
+__host__ __device__ inline int qc_index(int q, int x) { return (q * NXCD + x) * QC_STRIDE; }
+constexpr size_t QCOUNT_BYTES = (size_t)NQUEUE * NXCD * QC_STRIDE * 4;
 // hinfo bits of a primary hit record
 enum : uint32_t { HI_HIT = 1u, HI_UNDEF = 2u, HI_WATER = 4u, HI_SHADOWED = 8u, HI_NSHIFT = 4 };
 
@@ -48,7 +56,8 @@ struct FrameParams {
     float4* hsec;           // water colour (pre-fog) or summed cone light
     float4* pphit;          // half res: pre-pass hit position, w = normal code bits
     int* queue_wf[NQUEUE];
-    unsigned* qcount;       // NQUEUE counters, zeroed before every frame
+    unsigned* qcount;       // qc_index(q, xcd) counters, zeroed before every frame
+    uint32_t qcap[NQUEUE];  // items per XCD sub-queue (sub-queue x at queue_wf[q] + x * qcap[q])
     int enq;                // queue append: 0 one atomic per wave, 1 per workgroup
 };
 
@@ -67,6 +76,8 @@ void launch_csdf_export(hipStream_t s, const uint32_t* brick, uint8_t* canon, co
 void launch_gi_init(hipStream_t s, uint32_t* gi, const World& w, f3 sun, unsigned long long* counters);
 void launch_gi_update(hipStream_t s, const uint32_t* prev, uint32_t* next, const World& w, f3 sun,
                       uint32_t frame, uint64_t first, uint64_t count, unsigned long long* counters);
+// workgroups of the kernel that fills queue q (sizes its per-XCD sub-queues)
+uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
 void launch_prepass_tiles(hipStream_t s, const World& w, const FrameParams& f);

@@ -26,17 +26,20 @@
 namespace rv {
 
 // -------------------------------------------------------------- helpers
+// XCD of this workgroup under round-robin dispatch of linear workgroup ids
+__device__ __forceinline__ uint32_t my_xcd() { return (blockIdx.x + blockIdx.y * gridDim.x) & (NXCD - 1); }
+
 // Wave-aggregated append: one atomic per wave, slots in lane order.
 // Must be reached by every lane of the wave (pred false where not wanted).
-__device__ __forceinline__ void enqueue(int* q, unsigned* cnt, bool pred, int value) {
+__device__ __forceinline__ void enqueue(const FrameParams& f, int q, bool pred, int value) {
     const uint64_t m = __ballot(pred);
     if (m == 0) return;
-    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane = threadIdx.x & 63u, x = my_xcd();
     const int leader = __ffsll((unsigned long long)m) - 1;
     unsigned base = 0;
-    if ((int)lane == leader) base = atomicAdd(cnt, (unsigned)__popcll(m));
+    if ((int)lane == leader) base = atomicAdd(&f.qcount[qc_index(q, x)], (unsigned)__popcll(m));
     base = __shfl(base, leader);
-    if (pred) q[base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = value;
+    if (pred) f.queue_wf[q][(size_t)x * f.qcap[q] + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = value;
 }
 
 // Workgroup-aggregated append to NQ queues at once: one atomic per (workgroup,
@@ -48,7 +51,7 @@ __device__ __forceinline__ void enqueue_block(const FrameParams& f, const int (&
                                               int value) {
     __shared__ uint32_t s_n[NQ][4];
     __shared__ uint32_t s_base[NQ];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, x = my_xcd();
     const uint64_t below = (1ull << lane) - 1ull;
     uint64_t m[NQ];
 #pragma unroll
@@ -60,7 +63,7 @@ __device__ __forceinline__ void enqueue_block(const FrameParams& f, const int (&
     if (threadIdx.x < NQ) {
         const int i = (int)threadIdx.x;
         uint32_t tot = s_n[i][0] + s_n[i][1] + s_n[i][2] + s_n[i][3];
-        s_base[i] = tot ? atomicAdd(&f.qcount[qid[i]], tot) : 0u;
+        s_base[i] = tot ? atomicAdd(&f.qcount[qc_index(qid[i], x)], tot) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -68,9 +71,18 @@ __device__ __forceinline__ void enqueue_block(const FrameParams& f, const int (&
         if (pred[i]) {
             uint32_t off = s_base[i];
             for (uint32_t k = 0; k < wave; k++) off += s_n[i][k];
-            f.queue_wf[qid[i]][off + (uint32_t)__popcll(m[i] & below)] = value;
+            f.queue_wf[qid[i]][(size_t)x * f.qcap[qid[i]] + off + (uint32_t)__popcll(m[i] & below)] = value;
         }
     }
+}
+
+// Consumer side: workgroup b serves sub-queue b % 8 (the XCD it runs on),
+// items (b / 8) * 256 + tid.  False when this thread has no item.
+__device__ __forceinline__ bool queue_item(const FrameParams& f, int q, int& p) {
+    const uint32_t x = blockIdx.x & (NXCD - 1), k = (blockIdx.x / NXCD) * 256 + threadIdx.x;
+    if (k >= f.qcount[qc_index(q, x)]) return false;
+    p = f.queue_wf[q][(size_t)x * f.qcap[q] + k];
+    return true;
 }
 
 // normal (components in {-1, +1, +0}) <-> 3-bit code
@@ -152,16 +164,15 @@ __global__ void __launch_bounds__(256) k_wf_pp_primary(World w, FrameParams f) {
         }
     }
     if (f.enq) enqueue_block<1>(f, {Q_PP}, {hit}, p);
-    else enqueue(f.queue_wf[Q_PP], &f.qcount[Q_PP], hit, p);
+    else enqueue(f, Q_PP, hit, p);
     if (STATS) block_count_flush<NCNT>(f.counters, c);
 }
 
 template <bool STATS>
 __global__ void __launch_bounds__(256) k_wf_pp_shadow(World w, FrameParams f) {
     uint32_t c[NCNT] = {};
-    const unsigned n = f.qcount[Q_PP];
-    for (unsigned k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
-        int p = f.queue_wf[Q_PP][k];
+    int p;
+    if (queue_item(f, Q_PP, p)) {
         float4 hp = f.pphit[p];
         f3 pos = V(hp.x, hp.y, hp.z), nrm = normal_of(__float_as_uint(hp.w));
         StepCount sc{};
@@ -205,9 +216,9 @@ __global__ void __launch_bounds__(256) k_wf_primary(World w, FrameParams f) {
     if (f.enq) {
         enqueue_block<3>(f, {Q_WATER, Q_SHADOW, Q_CONE}, {water, shadow, cone}, p);
     } else {
-        enqueue(f.queue_wf[Q_WATER], &f.qcount[Q_WATER], water, p);
-        enqueue(f.queue_wf[Q_SHADOW], &f.qcount[Q_SHADOW], shadow, p);
-        enqueue(f.queue_wf[Q_CONE], &f.qcount[Q_CONE], cone, p);
+        enqueue(f, Q_WATER, water, p);
+        enqueue(f, Q_SHADOW, shadow, p);
+        enqueue(f, Q_CONE, cone, p);
     }
     if (STATS) block_count_flush<NCNT>(f.counters, c);
 }
@@ -216,9 +227,8 @@ __global__ void __launch_bounds__(256) k_wf_primary(World w, FrameParams f) {
 template <bool STATS>
 __global__ void __launch_bounds__(256) k_wf_shadow(World w, FrameParams f) {
     uint32_t c[NCNT] = {};
-    const unsigned n = f.qcount[Q_SHADOW];
-    for (unsigned k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
-        int p = f.queue_wf[Q_SHADOW][k];
+    int p;
+    if (queue_item(f, Q_SHADOW, p)) {
         float4 hp = f.hpos[p];
         uint32_t info = f.hinfo[p];
         f3 pos = V(hp.x, hp.y, hp.z), nrm = normal_of(info >> HI_NSHIFT);
@@ -237,9 +247,8 @@ __global__ void __launch_bounds__(256) k_wf_shadow(World w, FrameParams f) {
 template <bool STATS>
 __global__ void __launch_bounds__(256) k_wf_water(World w, FrameParams f) {
     uint32_t c[NCNT] = {};
-    const unsigned n = f.qcount[Q_WATER];
-    for (unsigned k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
-        int p = f.queue_wf[Q_WATER][k];
+    int p;
+    if (queue_item(f, Q_WATER, p)) {
         int ix = p % f.W, iy = p / f.W;
         float x = (float)ix / (float)f.W, y = (float)iy / (float)f.H;
         f3 dir = ray_dir(f, x, y);
@@ -275,9 +284,8 @@ __global__ void __launch_bounds__(256) k_wf_water(World w, FrameParams f) {
 template <bool STATS>
 __global__ void __launch_bounds__(256) k_wf_cones(World w, FrameParams f) {
     uint32_t c[NCNT] = {};
-    const unsigned n = f.qcount[Q_CONE];
-    for (unsigned k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
-        int p = f.queue_wf[Q_CONE][k];
+    int p;
+    if (queue_item(f, Q_CONE, p)) {
         float4 hp = f.hpos[p];
         f3 pos = V(hp.x, hp.y, hp.z), up = normal_of(f.hinfo[p] >> HI_NSHIFT);
         f3 right = normalize(cross(up, V(0.577f, 0.577f, 0.577f)));
@@ -384,16 +392,29 @@ __global__ void __launch_bounds__(256) k_wf_shade(World w, FrameParams f) {
 
 // ================================================================ launchers
 template <typename K>
-static void launch_queue_kernel(hipStream_t s, K kernel, const World& w, const FrameParams& f, uint32_t max_items) {
-    // One thread per possible item; the queue length is only known on the
-    // device, so blocks past it exit at once (a few us for a 2M-item bound).
-    uint32_t g = (max_items + 255) / 256;
-    if (g == 0) g = 1;
+static void launch_queue_kernel(hipStream_t s, K kernel, const World& w, const FrameParams& f, int q) {
+    // NXCD workgroups per 256 sub-queue slots; the queue lengths are only
+    // known on the device, so workgroups past them exit at once.
+    uint32_t g = NXCD * ((f.qcap[q] + 255) / 256);
+    if (g == 0) g = NXCD;
     hipLaunchKernelGGL(kernel, dim3(g), dim3(256), 0, s, w, f);
 }
 
 static uint32_t full_grid(const FrameParams& f, int W, int H) {
     return sched_grid(f.sched == SCHED_QUEUE ? SCHED_CHUNK : f.sched, (W + 15) >> 4, (H + 15) >> 4, 0);
+}
+
+uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles) {
+    FrameParams g = f;
+    if (g.sched == SCHED_QUEUE) g.sched = SCHED_CHUNK;
+    if (q == Q_PP) {
+        if (!tiles) return full_grid(g, f.hw, f.hh);
+        int T2 = f.tile_px / 2 + 2;
+        return (uint32_t)((T2 * T2 + 255) / 256) * (uint32_t)f.ntiles;
+    }
+    if (!tiles) return full_grid(g, f.W, f.H);
+    int nb = (f.tile_px + 15) >> 4;
+    return (uint32_t)(nb * nb) * (uint32_t)f.ntiles;
 }
 
 void launch_wf_pp_primary(hipStream_t s, const World& w, const FrameParams& f, bool tiles) {
@@ -414,9 +435,8 @@ void launch_wf_pp_primary(hipStream_t s, const World& w, const FrameParams& f, b
 }
 
 void launch_wf_pp_shadow(hipStream_t s, const World& w, const FrameParams& f) {
-    uint32_t mx = (uint32_t)(f.hw * f.hh);
-    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_pp_shadow<true>, w, f, mx);
-    else launch_queue_kernel(s, k_wf_pp_shadow<false>, w, f, mx);
+    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_pp_shadow<true>, w, f, Q_PP);
+    else launch_queue_kernel(s, k_wf_pp_shadow<false>, w, f, Q_PP);
 }
 
 void launch_wf_primary(hipStream_t s, const World& w, const FrameParams& f, bool tiles) {
@@ -437,21 +457,18 @@ void launch_wf_primary(hipStream_t s, const World& w, const FrameParams& f, bool
 }
 
 void launch_wf_shadow(hipStream_t s, const World& w, const FrameParams& f) {
-    uint32_t mx = (uint32_t)(f.W * f.H);
-    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_shadow<true>, w, f, mx);
-    else launch_queue_kernel(s, k_wf_shadow<false>, w, f, mx);
+    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_shadow<true>, w, f, Q_SHADOW);
+    else launch_queue_kernel(s, k_wf_shadow<false>, w, f, Q_SHADOW);
 }
 
 void launch_wf_water(hipStream_t s, const World& w, const FrameParams& f) {
-    uint32_t mx = (uint32_t)(f.W * f.H);
-    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_water<true>, w, f, mx);
-    else launch_queue_kernel(s, k_wf_water<false>, w, f, mx);
+    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_water<true>, w, f, Q_WATER);
+    else launch_queue_kernel(s, k_wf_water<false>, w, f, Q_WATER);
 }
 
 void launch_wf_cones(hipStream_t s, const World& w, const FrameParams& f) {
-    uint32_t mx = (uint32_t)(f.W * f.H);
-    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_cones<true>, w, f, mx);
-    else launch_queue_kernel(s, k_wf_cones<false>, w, f, mx);
+    if (f.flags & RV_F_STATS) launch_queue_kernel(s, k_wf_cones<true>, w, f, Q_CONE);
+    else launch_queue_kernel(s, k_wf_cones<false>, w, f, Q_CONE);
 }
 
 void launch_wf_shade(hipStream_t s, const World& w, const FrameParams& f, bool tiles) {

@@ -88,6 +88,14 @@ class StateRender:
     def set_stream(self, stream_handle: int):
         self._check(self._L.rv_set_stream(self._h, C.c_void_p(stream_handle)), "rv_set_stream")
 
+    def set_frame_path(self, path):
+        """RV_PATH_FUSED (per-pixel megakernels) or RV_PATH_WAVEFRONT (stage kernels)."""
+        p = {"fused": _lib.RV_PATH_FUSED, "wavefront": _lib.RV_PATH_WAVEFRONT}.get(path, path)
+        self._check(self._L.rv_set_frame_path(self._h, int(p)), "rv_set_frame_path")
+
+    def set_gi_async(self, on):
+        self._check(self._L.rv_set_gi_async(self._h, int(bool(on))), "rv_set_gi_async")
+
     def sync(self):
         self._check(self._L.rv_sync(self._h), "rv_sync")
 

@@ -209,15 +209,15 @@ def test_golden_fixtures(rv, atlas):
 
 
 @pytest.mark.parametrize("flags", [0, 8, 7])
-def test_wavefront_equals_per_pixel_path(rv, atlas, flags, monkeypatch):
+def test_wavefront_equals_per_pixel_path(rv, atlas, flags):
     """The wavefront stages and the per-pixel (megakernel) path are two
     schedules of the same arithmetic: images and counters are identical."""
     from rvgrt_amd.configs import TEST_POSES_128
     lg, W, H = 7, 320, 192
     out = {}
     for mk in ("0", "1"):
-        monkeypatch.setenv("RV_MEGAKERNEL", mk)
         r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+        r.set_frame_path("fused" if mk == "1" else "wavefront")
         for pose in ("P0", "P1"):
             cam, vp = rv.camera_from_pose(*TEST_POSES_128[pose], W, H)
             r.stats_reset()
@@ -230,3 +230,38 @@ def test_wavefront_equals_per_pixel_path(rv, atlas, flags, monkeypatch):
         for k in range(3):
             assert np.array_equal(a[k], b[k]), (pose, k)
         assert a[3] == b[3]
+
+
+def test_gi_async_update_matches_serial_and_oracle(rv, atlas, oracle_world):
+    """rv_update_gi_data on the side stream (overlapping the previous frame's
+    render) gives the same grid and images as the serial order, and the grid
+    matches the oracle's partial updates (RAYPS-style rolling offset)."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H, rays = 7, 320, 192, 5000
+    ow = oracle_world(lg, lg, lg, gi_sweeps=1)
+    n = len(ow.gi) // 4
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
+    res = {}
+    for on in (0, 1):
+        r = rv.StateRender((lg,) * 3, W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas, gi_rays_per_frame=rays)
+        r.world_build()
+        r.gi_update(0)
+        r.set_gi_async(on)
+        imgs = []
+        for k in range(9):          # wraps the rolling offset once (32768 cells)
+            r.update_gi_data()
+            r.frame(cam, vp)
+            # read back every 4th frame only, so most updates are queued
+            # behind a still-running render
+            imgs.append(r.readback(rv.RV_IMAGE_COLOR).copy() if k % 4 == 0 else None)
+        r.sync()
+        res[on] = (r.world_export(rv.RV_WORLD_GI), imgs)
+        r.close()
+    assert np.array_equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a is None and b is None) or np.array_equal(a, b)
+    off = 0
+    for k in range(9):              # oracle: the same rolling partial updates
+        ow.gi_update(k, first=off, count=min(rays, n - off))
+        off = 0 if off + rays >= n else off + rays
+    assert np.array_equal(res[1][0], ow.gi)
