@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librvgrt_hip.so")
+# RVGRT_LIB: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("RVGRT_LIB") or os.path.join(_HERE, "librvgrt_hip.so")
 
 RV_OK, RV_ERR_INVALID, RV_ERR_HIP, RV_ERR_OOM, RV_ERR_STATE, RV_ERR_NO_DEVICE = range(6)
 RV_F_PREPASS, RV_F_WATER, RV_F_GI, RV_F_SHADOW, RV_F_STATS = 1, 2, 4, 8, 16

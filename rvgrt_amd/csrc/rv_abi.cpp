@@ -11,7 +11,7 @@
 #include <string>
 #include <vector>
 
-#include "rv_internal.h"
+#include "rv_frame.h"
 
 using namespace rv;
 
@@ -55,11 +55,14 @@ struct rv_ctx {
     int* wq[NQUEUE] = {nullptr, nullptr, nullptr, nullptr};
     size_t wq_cap[NQUEUE] = {0, 0, 0, 0};   // items allocated per queue (all sub-queues)
     unsigned* qcount = nullptr;
+    uint32_t* wtrace = nullptr;   // RV_WAVE_TRACE builds: per-wave records of the last k_render
+    size_t wtrace_bytes = 0;
     uint32_t gi_frame = 0;
     uint64_t gi_offset = 0;
     bool world_ready = false;
-    int sched = SCHED_CHUNK;
-    unsigned* queue = nullptr;   // work counters for SCHED_QUEUE
+    int sched = SCHED_COST;
+    int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
+    uint32_t* chunk_cost[2] = {nullptr, nullptr};
     std::string err;
 };
 
@@ -187,8 +190,19 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     hipMemset(c->hdist, 0, hbytes);
     hipMemset(c->hshadow, 0, hbytes);
     if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
-    if (hipMalloc(&c->queue, 16) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "queue");
-    hipMemset(c->queue, 0, 16);
+    {   // SCHED_COST chunk order (identity until a frame has been timed) and costs
+        const uint32_t nb[2][2] = {{(uint32_t)(W / 2), (uint32_t)(H / 2)}, {(uint32_t)W, (uint32_t)H}};
+        for (int g = 0; g < 2; g++) {
+            uint32_t npad = n_chunks_pad(nb[g][0], nb[g][1]);
+            std::vector<int> id(npad);
+            for (uint32_t i = 0; i < npad; i++) id[i] = (int)i;
+            if (hipMalloc(&c->chunk_order[g], npad * 4) != hipSuccess ||
+                hipMalloc(&c->chunk_cost[g], npad * 4) != hipSuccess)
+                return cleanup_fail(RV_ERR_OOM, "chunk order");
+            hipMemcpy(c->chunk_order[g], id.data(), npad * 4, hipMemcpyHostToDevice);
+            hipMemset(c->chunk_cost[g], 0, npad * 4);
+        }
+    }
     if (hipMalloc(&c->counters, NSTAGE * NCNT * sizeof(unsigned long long)) != hipSuccess)
         return cleanup_fail(RV_ERR_OOM, "counters");
     hipMemset(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long));
@@ -202,6 +216,13 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
         if (!ok) return cleanup_fail(RV_ERR_OOM, "wavefront buffers");
         hipMemset(c->qcount, 0, QCOUNT_BYTES);   // queues themselves: sized per frame by ensure_queues
     }
+#ifdef RV_WAVE_TRACE
+    if (getenv("RV_WAVE_TRACE")) {
+        c->wtrace_bytes = (size_t)sched_grid<8>(SCHED_COST, W, H) * 32;   // one 32-B record per wave
+        if (hipMalloc(&c->wtrace, c->wtrace_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "wave trace");
+        hipMemset(c->wtrace, 0, c->wtrace_bytes);
+    }
+#endif
     if (hipEventCreateWithFlags(&c->ev_world, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gi_done, hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&c->gi_stream, hipStreamNonBlocking) != hipSuccess)
@@ -218,10 +239,20 @@ void rv_destroy(rv_ctx* c) {
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
     hipFree(c->own_color); hipFree(c->own_mv); hipFree(c->own_depth);
     hipFree(c->hdist); hipFree(c->hshadow); hipFree(c->counters);
-    hipFree(c->tile_ids); hipFree(c->tilebuf); hipFree(c->queue);
+    hipFree(c->tile_ids); hipFree(c->tilebuf);
+    for (int g = 0; g < 2; g++) { hipFree(c->chunk_order[g]); hipFree(c->chunk_cost[g]); }
     hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
     for (int q = 0; q < NQUEUE; q++) hipFree(c->wq[q]);
     for (hipEvent_t e : c->ev) hipEventDestroy(e);
+#ifdef RV_WAVE_TRACE
+    if (c->wtrace) {   // env RV_WAVE_TRACE=<file>: dump the last frame's wave records
+        std::vector<uint32_t> h(c->wtrace_bytes / 4);
+        if (hipMemcpy(h.data(), c->wtrace, c->wtrace_bytes, hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE* fp = fopen(getenv("RV_WAVE_TRACE"), "wb")) { fwrite(h.data(), 4, h.size(), fp); fclose(fp); }
+        }
+        hipFree(c->wtrace);
+    }
+#endif
     if (c->gi_stream) { hipStreamSynchronize(c->gi_stream); hipStreamDestroy(c->gi_stream); }
     if (c->ev_world) hipEventDestroy(c->ev_world);
     if (c->ev_gi_done) hipEventDestroy(c->ev_gi_done);
@@ -427,11 +458,12 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
     f.hdist = c->hdist; f.hshadow = c->hshadow;
     f.counters = c->counters;
     f.sched = c->sched;
-    f.queue = c->queue;
+    for (int g = 0; g < 2; g++) { f.chunk_order[g] = c->chunk_order[g]; f.chunk_cost[g] = c->chunk_cost[g]; }
     f.hpos = c->hpos; f.hinfo = c->hinfo; f.hsec = c->hsec; f.pphit = c->pphit;
     for (int q = 0; q < NQUEUE; q++) f.queue_wf[q] = c->wq[q];
     f.qcount = c->qcount;
     f.enq = c->enq;
+    f.wtrace = c->wtrace;
     return f;
 }
 
@@ -469,7 +501,6 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
     auto stage = [&](int k) { FrameParams g = f; g.counters = c->counters + (size_t)k * NCNT; return g; };
     const bool pre = (f.flags & RV_F_PREPASS) != 0;
     if (c->megakernel) {
-        if (c->sched == SCHED_QUEUE) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 16, c->stream));
         HIP_TRY(c, mark(ST_PP_PRIMARY));
         if (pre) {
             if (tiles) launch_prepass_tiles(c->stream, w, stage(ST_PP_PRIMARY));
@@ -480,6 +511,11 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
         if (tiles) launch_render_tiles(c->stream, w, stage(ST_PRIMARY)); else launch_render(c->stream, w, stage(ST_PRIMARY));
         LAUNCH_CHECK(c);
         for (int k = ST_SHADOW; k <= ST_SHADE + 1; k++) HIP_TRY(c, mark(k));
+        if (!tiles) {   // SCHED_COST: next frame's chunk order from this frame's wave lifetimes
+            if (pre) launch_chunk_order(c->stream, f, CG_PREPASS, f.hw, f.hh);
+            launch_chunk_order(c->stream, f, CG_RENDER, f.W, f.H);
+            LAUNCH_CHECK(c);
+        }
     } else {
         HIP_TRY(c, hipMemsetAsync(c->qcount, 0, QCOUNT_BYTES, c->stream));
         HIP_TRY(c, mark(ST_PP_PRIMARY));

@@ -264,6 +264,7 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 //   * the DDA loop has one exit (a status code); the jump and the hit
 //     record are computed after it, so the per-step body is one 4-B gather
 //     plus ~20 VALU instructions.
+
 template <bool COUNT>
 __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
@@ -290,9 +291,10 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
         for (int it = 0; it < 100; it++) {
             int fx = (int)floorf(cur.x), fy = (int)floorf(cur.y), fz = (int)floorf(cur.z);
             oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= Y) | ((uint32_t)fz >= Z);
-            uint32_t d = csdf_at(w, min((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u),
-                                 min((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u),
-                                 min((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u));
+            const uint32_t cx = min((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
+            const uint32_t cy = min((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
+            const uint32_t cz = min((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
+            const uint32_t d = csdf_at(w, (int)cx, (int)cy, (int)cz);
             if (COUNT) sc.sphere += !oob;
             const bool stop = oob | (d <= 1);
             f3 nxt = add(cur, scale(dir, (float)d));
@@ -312,17 +314,17 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
         uint32_t jd = 0;
         for (int i = 0; i < 200; i++) {
             if ((i & 7) == 7) {   // i is wave-uniform: a scalar branch
-                int cx = min(max(ix >> 1, 0), w.SX - 1);
-                int cy = min(max(iy >> 1, 0), w.SY - 1);
-                int cz = min(max(iz >> 1, 0), w.SZ - 1);
-                jd = csdf_at(w, cx, cy, cz);
+                uint32_t cx = (uint32_t)min(max(ix >> 1, 0), w.SX - 1);
+                uint32_t cy = (uint32_t)min(max(iy >> 1, 0), w.SY - 1);
+                uint32_t cz = (uint32_t)min(max(iz >> 1, 0), w.SZ - 1);
+                jd = csdf_at(w, (int)cx, (int)cy, (int)cz);
                 if (COUNT) sc.check++;
                 st = jd > 2 ? 1 : 0;
             }
             const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
             // clamped (always valid) gather; its bit only counts in bounds
-            uint32_t word = load_dword(w, voxel_word_off(w, min((uint32_t)ix, X - 1u), min((uint32_t)iy, Y - 1u),
-                                                         min((uint32_t)iz, Z - 1u)));
+            const uint32_t qx = min((uint32_t)ix, X - 1u), qy = min((uint32_t)iy, Y - 1u), qz = min((uint32_t)iz, Z - 1u);
+            const uint32_t word = load_dword(w, voxel_word_off(w, qx, qy, qz));
             const bool solid = (word >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
             if (COUNT) sc.dda += (st == 0) & !oob;
             st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));

@@ -41,57 +41,56 @@ __device__ __forceinline__ f3 ray_dir(const FrameParams& f, float x, float y) {
 //                    sky/terrain cost gradient makes the bands unequal)
 //   SCHED_CHUNK    : 4x4-block chunks (64x64 px) dealt round-robin to XCDs:
 //                    locality inside a chunk, balance across XCDs
-//   SCHED_QUEUE    : persistent workgroups pull blocks (chunk order) from an
-//                    atomic counter until the frame is drained
-__device__ __forceinline__ bool chunk_block(uint32_t k, uint32_t nbx, uint32_t nby, uint32_t& bx,
+//   SCHED_COST     : SCHED_CHUNK with the chunks dealt in descending order of
+//                    their cost in the previous frame (longest-job-first), so
+//                    the waves with the longest rays start first instead of
+//                    forming the kernel's tail (chunk_order; identity at first)
+static constexpr uint32_t CHUNK_PX = 64;   // chunk = 64 x 64 pixels
+
+__host__ __device__ inline uint32_t chunks_x(uint32_t w) { return (w + CHUNK_PX - 1) / CHUNK_PX; }
+__host__ __device__ inline uint32_t n_chunks(uint32_t w, uint32_t h) { return chunks_x(w) * chunks_x(h); }
+__host__ __device__ inline uint32_t n_chunks_pad(uint32_t w, uint32_t h) { return (n_chunks(w, h) + 7) & ~7u; }
+
+// Grid of BS x BS-pixel workgroup tiles over a w x h image.
+template <uint32_t BS>
+__host__ __device__ inline uint32_t sched_grid(int sched, uint32_t w, uint32_t h) {
+    constexpr uint32_t CBS = CHUNK_PX / BS;
+    if (sched == SCHED_CHUNK || sched == SCHED_COST) return n_chunks_pad(w, h) * CBS * CBS;
+    return ((w + BS - 1) / BS) * ((h + BS - 1) / BS);
+}
+
+// Tile (bx, by) of this workgroup; false for the padding workgroups of a
+// chunked grid and for tiles off the image.
+template <uint32_t BS>
+__device__ __forceinline__ bool sched_block(int sched, const int* order, uint32_t w, uint32_t h, uint32_t& bx,
                                             uint32_t& by) {
-    const uint32_t CB = 4;
-    uint32_t ncx = (nbx + CB - 1) / CB;
-    uint32_t chunk = k / (CB * CB), j = k % (CB * CB);
-    bx = (chunk % ncx) * CB + j % CB;
-    by = (chunk / ncx) * CB + j / CB;
-    return bx < nbx && by < nby;
-}
-
-__host__ __device__ inline uint32_t sched_grid(int sched, uint32_t nbx, uint32_t nby, uint32_t persistent) {
-    const uint32_t CB = 4;
-    uint32_t nch = ((nbx + CB - 1) / CB) * ((nby + CB - 1) / CB);
-    switch (sched) {
-    case SCHED_CHUNK: return ((nch + 7) & ~7u) * CB * CB;
-    case SCHED_QUEUE: return persistent;
-    default: return nbx * nby;
-    }
-}
-
-// Returns the next block of this workgroup (uniform across it), false when done.
-__device__ __forceinline__ bool sched_next(int sched, unsigned* queue, uint32_t nbx, uint32_t nby,
-                                           uint32_t& iter, uint32_t& bx, uint32_t& by) {
-    if (sched == SCHED_QUEUE) {
-        __shared__ uint32_t s_k;
-        const uint32_t CB = 4;
-        uint32_t total = ((nbx + CB - 1) / CB) * ((nby + CB - 1) / CB) * CB * CB;
-        for (;;) {
-            __syncthreads();
-            if (threadIdx.x == 0) s_k = atomicAdd(queue, 1u);
-            __syncthreads();
-            uint32_t k = s_k;
-            if (k >= total) return false;
-            if (chunk_block(k, nbx, nby, bx, by)) return true;
-        }
-    }
-    if (iter++ > 0) return false;
+    constexpr uint32_t CBS = CHUNK_PX / BS;
+    const uint32_t nbx = (w + BS - 1) / BS, nby = (h + BS - 1) / BS;
     uint32_t b = blockIdx.x;
-    if (sched == SCHED_BAND) {
-        b = xcd_swizzle(b, nbx * nby);
-    } else if (sched == SCHED_CHUNK) {
-        const uint32_t CB = 4;
+    if (sched == SCHED_CHUNK || sched == SCHED_COST) {
+        // workgroup b runs on XCD b % 8: slot k of that XCD takes sorted chunk
+        // (k / CBS^2) * 8 + xcd, tile k % CBS^2 inside it
         uint32_t xcd = b & 7u, k = b >> 3;
-        uint32_t chunk = (k / (CB * CB)) * 8 + xcd;
-        return chunk_block(chunk * CB * CB + k % (CB * CB), nbx, nby, bx, by);
+        uint32_t pos = (k / (CBS * CBS)) * 8 + xcd;
+        uint32_t chunk = (sched == SCHED_COST && order) ? (uint32_t)order[pos] : pos;
+        uint32_t j = k % (CBS * CBS), ncx = chunks_x(w);
+        bx = (chunk % ncx) * CBS + j % CBS;
+        by = (chunk / ncx) * CBS + j / CBS;
+        return bx < nbx && by < nby;
     }
+    if (sched == SCHED_BAND) b = xcd_swizzle(b, nbx * nby);
     bx = b % nbx;
     by = b / nbx;
     return by < nby;
+}
+
+// SCHED_COST feedback: every wave reports its lifetime to its chunk.
+template <uint32_t BS>
+__device__ __forceinline__ void chunk_cost_report(uint32_t* cost, uint64_t t0, uint32_t w, uint32_t bx, uint32_t by) {
+    if (!cost || (threadIdx.x & 63) != 0) return;
+    uint64_t dt = wall_clock64() - t0;
+    atomicMax(&cost[(by * BS / CHUNK_PX) * chunks_x(w) + bx * BS / CHUNK_PX],
+              (uint32_t)(dt > 0xFFFFFFFEull ? 0xFFFFFFFEull : dt) + 1u);
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -121,16 +120,5 @@ __device__ __forceinline__ float bilinear_tex(const FrameParams& f, float x, flo
     float t01 = hs[(size_t)j1 * f.hw + i0], t11 = hs[(size_t)j1 * f.hw + i1];
     return (1.0f - a) * (1.0f - b) * t00 + a * (1.0f - b) * t10 + (1.0f - a) * b * t01 + a * b * t11;
 }
-
-// resident workgroups for a persistent launch: occupancy x CUs
-template <typename K>
-inline uint32_t resident_blocks(K kernel) {
-    int dev = 0, ncu = 256, per = 1;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0);
-    return (uint32_t)(ncu * (per > 0 ? per : 1));
-}
-
 
 }  // namespace rv

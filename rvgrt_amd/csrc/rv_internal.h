@@ -17,7 +17,9 @@ enum {
 };
 
 // workgroup -> pixel-block scheduling of the frame kernels (see rv_kernels.hip)
-enum { SCHED_IDENTITY = 0, SCHED_BAND = 1, SCHED_CHUNK = 2, SCHED_QUEUE = 3 };
+enum { SCHED_IDENTITY = 0, SCHED_BAND = 1, SCHED_CHUNK = 2, SCHED_COST = 3 };
+// SCHED_COST chunk feedback: [0] pre-pass grid, [1] render grid
+enum { CG_PREPASS = 0, CG_RENDER = 1 };
 
 // Frame stages: one counter block (RV_F_STATS) and one timing slot each.
 // Wavefront path: PP_PRIMARY, PP_SHADOW, PRIMARY, SHADOW, WATER, CONES, SHADE;
@@ -38,7 +40,8 @@ enum : uint32_t { HI_HIT = 1u, HI_UNDEF = 2u, HI_WATER = 4u, HI_SHADOWED = 8u, H
 
 struct FrameParams {
     int sched;
-    unsigned* queue;   // [0] pre-pass, [1] render work counters (SCHED_QUEUE)
+    const int* chunk_order[2];   // SCHED_COST: chunks by descending cost of the last frame (CG_*)
+    uint32_t* chunk_cost[2];     // SCHED_COST: this frame's max wave lifetime per chunk (10 ns ticks)
     f3 pos, fo, ri, up, sun;
     float time, jx, jy;
     float vp[16], pvp[16];
@@ -59,6 +62,7 @@ struct FrameParams {
     unsigned* qcount;       // qc_index(q, xcd) counters, zeroed before every frame
     uint32_t qcap[NQUEUE];  // items per XCD sub-queue (sub-queue x at queue_wf[q] + x * qcap[q])
     int enq;                // queue append: 0 one atomic per wave, 1 per workgroup
+    uint32_t* wtrace;       // RV_WAVE_TRACE builds: 8 dwords per k_render wave (diagnostics)
 };
 
 struct RvHitDev {   // == rv_hit
@@ -80,6 +84,8 @@ void launch_gi_update(hipStream_t s, const uint32_t* prev, uint32_t* next, const
 uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
+// SCHED_COST: sort the chunk costs of grid g into chunk_order and clear them
+void launch_chunk_order(hipStream_t s, const FrameParams& f, int g, uint32_t w, uint32_t h);
 void launch_prepass_tiles(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render_tiles(hipStream_t s, const World& w, const FrameParams& f);
 // wavefront stages (rv_wavefront.hip); `counters` of f must point at the

@@ -123,8 +123,7 @@ __device__ __forceinline__ bool pixel_of(const FrameParams& f, int W, int H, int
         ix = tx * T + lx; iy = ty * T + ly;
         return lx < T && ly < T && ix < W && iy < H;
     }
-    uint32_t it = 0;
-    if (!sched_next(f.sched, nullptr, (W + 15) >> 4, (H + 15) >> 4, it, bx, by)) { ix = iy = 0; return false; }
+    if (!sched_block<16>(f.sched, nullptr, W, H, bx, by)) { ix = iy = 0; return false; }
     ix = (int)(bx * 16 + (wave & 1) * 8 + (lane & 7));
     iy = (int)(by * 16 + (wave >> 1) * 8 + (lane >> 3));
     return ix < W && iy < H;
@@ -401,12 +400,12 @@ static void launch_queue_kernel(hipStream_t s, K kernel, const World& w, const F
 }
 
 static uint32_t full_grid(const FrameParams& f, int W, int H) {
-    return sched_grid(f.sched == SCHED_QUEUE ? SCHED_CHUNK : f.sched, (W + 15) >> 4, (H + 15) >> 4, 0);
+    return sched_grid<16>(f.sched, W, H);
 }
 
 uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles) {
     FrameParams g = f;
-    if (g.sched == SCHED_QUEUE) g.sched = SCHED_CHUNK;
+    if (g.sched == SCHED_COST) g.sched = SCHED_CHUNK;   // no cost feedback for the stage kernels
     if (q == Q_PP) {
         if (!tiles) return full_grid(g, f.hw, f.hh);
         int T2 = f.tile_px / 2 + 2;
@@ -420,7 +419,7 @@ uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles) {
 void launch_wf_pp_primary(hipStream_t s, const World& w, const FrameParams& f, bool tiles) {
     const bool st = (f.flags & RV_F_STATS) != 0;
     FrameParams g = f;
-    if (g.sched == SCHED_QUEUE) g.sched = SCHED_CHUNK;
+    if (g.sched == SCHED_COST) g.sched = SCHED_CHUNK;   // no cost feedback for the stage kernels
     if (tiles) {
         if (f.ntiles <= 0) return;
         int T2 = f.tile_px / 2 + 2;
@@ -442,7 +441,7 @@ void launch_wf_pp_shadow(hipStream_t s, const World& w, const FrameParams& f) {
 void launch_wf_primary(hipStream_t s, const World& w, const FrameParams& f, bool tiles) {
     const bool st = (f.flags & RV_F_STATS) != 0;
     FrameParams g = f;
-    if (g.sched == SCHED_QUEUE) g.sched = SCHED_CHUNK;
+    if (g.sched == SCHED_COST) g.sched = SCHED_CHUNK;   // no cost feedback for the stage kernels
     if (tiles) {
         if (f.ntiles <= 0) return;
         int nb = (f.tile_px + 15) >> 4;
@@ -474,7 +473,7 @@ void launch_wf_cones(hipStream_t s, const World& w, const FrameParams& f) {
 void launch_wf_shade(hipStream_t s, const World& w, const FrameParams& f, bool tiles) {
     const bool st = (f.flags & RV_F_STATS) != 0;
     FrameParams g = f;
-    if (g.sched == SCHED_QUEUE) g.sched = SCHED_CHUNK;
+    if (g.sched == SCHED_COST) g.sched = SCHED_CHUNK;   // no cost feedback for the stage kernels
     if (tiles) {
         if (f.ntiles <= 0) return;
         int nb = (f.tile_px + 15) >> 4;
