@@ -43,6 +43,8 @@ struct rv_ctx {
     int timing_cap = 0, timing_n = 0;
     std::vector<hipEvent_t> ev;
     std::vector<char> gi_timed;
+    std::vector<signed char> ev_stage;   // stage of each frame event slot (-1: end of frame)
+    std::vector<int> ev_used;            // frame event slots used per frame
     bool megakernel = true;       // RV_PATH_FUSED (k_prepass/k_render); false: wavefront stages
     // asynchronous GI update (rv_set_gi_async): kernel on gi_stream, copy-back on stream
     bool gi_async = true;
@@ -61,6 +63,8 @@ struct rv_ctx {
     uint64_t gi_offset = 0;
     bool world_ready = false;
     int sched = SCHED_COST;
+    int order_every = 4;          // RV_ORDER_EVERY: frames between chunk re-orderings
+    uint32_t frames_since_order = 0;
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
     uint32_t* chunk_cost[2] = {nullptr, nullptr};
     std::string err;
@@ -146,6 +150,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
     c->brick_bytes = ((uint64_t)w.X * w.Y * w.Z) / 4;   // 128 B per 512 voxels
+    w.coff = csdf_region(((uint64_t)w.X * w.Y * w.Z) / 512);
     c->gi_bytes = n_gi(c) * 4;
 
     auto cleanup_fail = [&](rv_status s, const char* what) {
@@ -190,6 +195,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     hipMemset(c->hdist, 0, hbytes);
     hipMemset(c->hshadow, 0, hbytes);
     if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
+    if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     {   // SCHED_COST chunk order (identity until a frame has been timed) and costs
         const uint32_t nb[2][2] = {{(uint32_t)(W / 2), (uint32_t)(H / 2)}, {(uint32_t)W, (uint32_t)H}};
         for (int g = 0; g < 2; g++) {
@@ -494,48 +500,73 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
         rv_status st = ensure_queues(c, f, tiles);
         if (st != RV_OK) return st;
     }
+    // Stage timing: one event where a stage starts and one at the end of
+    // the frame, on the stages that run (an event costs a few us of gap).
     const bool timed = c->timing_n < c->timing_cap;
-    hipEvent_t* e = timed ? &c->ev[(size_t)EV_PER_FRAME * c->timing_n] : nullptr;
+    const size_t e0 = (size_t)EV_PER_FRAME * c->timing_n;
+    int used = 0;
+    auto mark = [&](int k) -> hipError_t {
+        if (!timed) return hipSuccess;
+        c->ev_stage[e0 + used] = (signed char)k;
+        return hipEventRecord(c->ev[e0 + used++], c->stream);
+    };
     World w = current_world(c);
-    auto mark = [&](int k) -> hipError_t { return timed ? hipEventRecord(e[k], c->stream) : hipSuccess; };
     auto stage = [&](int k) { FrameParams g = f; g.counters = c->counters + (size_t)k * NCNT; return g; };
     const bool pre = (f.flags & RV_F_PREPASS) != 0;
     if (c->megakernel) {
-        HIP_TRY(c, mark(ST_PP_PRIMARY));
         if (pre) {
+            HIP_TRY(c, mark(ST_PP_PRIMARY));
             if (tiles) launch_prepass_tiles(c->stream, w, stage(ST_PP_PRIMARY));
             else launch_prepass(c->stream, w, stage(ST_PP_PRIMARY));
             LAUNCH_CHECK(c);
         }
-        for (int k = ST_PP_SHADOW; k <= ST_PRIMARY; k++) HIP_TRY(c, mark(k));
+        HIP_TRY(c, mark(ST_PRIMARY));
         if (tiles) launch_render_tiles(c->stream, w, stage(ST_PRIMARY)); else launch_render(c->stream, w, stage(ST_PRIMARY));
         LAUNCH_CHECK(c);
-        for (int k = ST_SHADOW; k <= ST_SHADE + 1; k++) HIP_TRY(c, mark(k));
-        if (!tiles) {   // SCHED_COST: next frame's chunk order from this frame's wave lifetimes
+        HIP_TRY(c, mark(-1));
+        // SCHED_COST: re-order the chunks by the wave lifetimes (max over
+        // the frames since the last ordering) every order_every frames; a
+        // kernel boundary costs ~6 us, the ordering itself ~4 us.
+        if (!tiles && ++c->frames_since_order >= (uint32_t)c->order_every) {
+            c->frames_since_order = 0;
             if (pre) launch_chunk_order(c->stream, f, CG_PREPASS, f.hw, f.hh);
             launch_chunk_order(c->stream, f, CG_RENDER, f.W, f.H);
             LAUNCH_CHECK(c);
         }
     } else {
         HIP_TRY(c, hipMemsetAsync(c->qcount, 0, QCOUNT_BYTES, c->stream));
-        HIP_TRY(c, mark(ST_PP_PRIMARY));
-        if (pre) { launch_wf_pp_primary(c->stream, w, stage(ST_PP_PRIMARY), tiles); LAUNCH_CHECK(c); }
-        HIP_TRY(c, mark(ST_PP_SHADOW));
-        if (pre) { launch_wf_pp_shadow(c->stream, w, stage(ST_PP_SHADOW)); LAUNCH_CHECK(c); }
+        if (pre) {
+            HIP_TRY(c, mark(ST_PP_PRIMARY));
+            launch_wf_pp_primary(c->stream, w, stage(ST_PP_PRIMARY), tiles);
+            LAUNCH_CHECK(c);
+            HIP_TRY(c, mark(ST_PP_SHADOW));
+            launch_wf_pp_shadow(c->stream, w, stage(ST_PP_SHADOW));
+            LAUNCH_CHECK(c);
+        }
         HIP_TRY(c, mark(ST_PRIMARY));
         launch_wf_primary(c->stream, w, stage(ST_PRIMARY), tiles);
         LAUNCH_CHECK(c);
-        HIP_TRY(c, mark(ST_SHADOW));
-        if (!pre && (f.flags & RV_F_SHADOW)) { launch_wf_shadow(c->stream, w, stage(ST_SHADOW)); LAUNCH_CHECK(c); }
-        HIP_TRY(c, mark(ST_WATER));
-        if (f.flags & RV_F_WATER) { launch_wf_water(c->stream, w, stage(ST_WATER)); LAUNCH_CHECK(c); }
-        HIP_TRY(c, mark(ST_CONES));
-        if (f.flags & RV_F_GI) { launch_wf_cones(c->stream, w, stage(ST_CONES)); LAUNCH_CHECK(c); }
+        if (!pre && (f.flags & RV_F_SHADOW)) {
+            HIP_TRY(c, mark(ST_SHADOW));
+            launch_wf_shadow(c->stream, w, stage(ST_SHADOW));
+            LAUNCH_CHECK(c);
+        }
+        if (f.flags & RV_F_WATER) {
+            HIP_TRY(c, mark(ST_WATER));
+            launch_wf_water(c->stream, w, stage(ST_WATER));
+            LAUNCH_CHECK(c);
+        }
+        if (f.flags & RV_F_GI) {
+            HIP_TRY(c, mark(ST_CONES));
+            launch_wf_cones(c->stream, w, stage(ST_CONES));
+            LAUNCH_CHECK(c);
+        }
         HIP_TRY(c, mark(ST_SHADE));
         launch_wf_shade(c->stream, w, stage(ST_SHADE), tiles);
         LAUNCH_CHECK(c);
-        HIP_TRY(c, mark(ST_SHADE + 1));
+        HIP_TRY(c, mark(-1));
     }
+    if (timed) c->ev_used[c->timing_n] = used;
     if (timed) c->timing_n++;
     return RV_OK;
 }
@@ -621,6 +652,8 @@ rv_status rv_timing_enable(rv_ctx* c, int32_t max_frames) {
     c->timing_cap = 0; c->timing_n = 0;
     c->ev.resize((size_t)max_frames * EV_PER_FRAME);
     c->gi_timed.assign((size_t)max_frames, 0);
+    c->ev_stage.assign((size_t)max_frames * EV_PER_FRAME, -1);
+    c->ev_used.assign((size_t)max_frames, 0);
     for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
     c->timing_cap = max_frames;
     return RV_OK;
@@ -631,11 +664,13 @@ rv_status rv_timing_stages(rv_ctx* c, double* ms, int32_t n, int32_t* frames) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < n; k++) ms[k] = 0.0;
     for (int i = 0; i < c->timing_n; i++) {
-        hipEvent_t* e = &c->ev[(size_t)EV_PER_FRAME * i];
-        for (int k = 0; k < NSTAGE - 1 && k < n; k++) {
+        const size_t e0 = (size_t)EV_PER_FRAME * i;
+        hipEvent_t* e = &c->ev[e0];
+        for (int j = 0; j + 1 < c->ev_used[i]; j++) {
+            const int k = c->ev_stage[e0 + j];
             float t = 0.0f;
-            HIP_TRY(c, hipEventElapsedTime(&t, e[k], e[k + 1]));
-            ms[k] += t;
+            HIP_TRY(c, hipEventElapsedTime(&t, e[j], e[j + 1]));
+            if (k >= 0 && k < n) ms[k] += t;
         }
         if (c->gi_timed[i] && ST_GI < n) {
             float t = 0.0f;
