@@ -58,8 +58,10 @@ def algorithmic_bytes(st: dict, px: int, halfpx: int, prepass: bool, stage: str,
         b += (st["cones"] // 6) * (4 + 20 + 16)
     elif stage == "shade":
         b += px * (20 + 10 + (16 if prepass else 0))
-    elif stage == "frame":   # the whole fused frame (per-pixel path)
-        b += px * (10 + (32 if prepass else 0)) + (halfpx * 8 if prepass else 0)
+    elif stage == "fused_prepass":   # k_prepass: 4 B distance + 4 B shadow per half-res pixel
+        b += halfpx * 8
+    elif stage == "fused_render":    # k_render: 10 B outputs; 4 min-dist + 4 bilinear taps (32 B)
+        b += px * (10 + (32 if prepass else 0))
     return int(b)
 
 
@@ -71,7 +73,7 @@ def main():
     ap.add_argument("--config", default="c2", help="c1..c5 (default c2 = BASELINE configs[1])")
     ap.add_argument("--pose", default="P0")
     ap.add_argument("--tile-px", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+    ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
     ap.add_argument("--path", default="fused", choices=["fused", "wavefront"],
@@ -135,7 +137,8 @@ def main():
     megakernel = args.path == "fused"
     pp_hits = st_stage["pp_shadow"]["prepass_shadow"]
     stage_bytes = {name: algorithmic_bytes(st_stage[name], W * H, (W // 2) * (H // 2), prepass,
-                                           "frame" if megakernel and name in ("pp_primary", "primary") else name,
+                                           {"pp_primary": "fused_prepass", "primary": "fused_render"}.get(name, name)
+                                           if megakernel else name,
                                            pp_hits)
                    for name in rv._lib.STAGES if name != "gi"}
 
@@ -291,16 +294,20 @@ def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
     order = [s for k in range(4) for s in starts[k::4]]
     t0 = time.perf_counter()
     rays = rows = 0
-    for s in order:
-        out = O.render(w, fr, s, min(H, s + band))
-        rays += out["stats"]["traces"]
-        rows += min(H, s + band) - s
-        if time.perf_counter() - t0 >= budget_s:
-            break
+    done = False
+    while not done:            # whole frames (row bands in a spread order) until the budget is spent
+        for s in order:
+            out = O.render(w, fr, s, min(H, s + band))
+            rays += out["stats"]["traces"]
+            rows += min(H, s + band) - s
+            if time.perf_counter() - t0 >= budget_s:
+                done = True
+                break
     dt = time.perf_counter() - t0
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/rv_oracle.c render of {rows}/{H} rows of {cfg.name} in {band}-row bands "
-                      f"({dt:.1f}s, {rays} traces), same world/camera/flags"}
+            "sample": f"oracle/rv_oracle.c render of {rows} rows ({rows / H:.2f} frames) of {cfg.name} in "
+                      f"{band}-row bands on {threads} threads ({dt:.1f}s wall, {rays} traces), "
+                      "same world/camera/flags"}
 
 
 if __name__ == "__main__":
