@@ -79,6 +79,9 @@ def main():
     ap.add_argument("--path", default="fused", choices=["fused", "wavefront"],
                     help="frame path: per-pixel megakernels (default) or wavefront stage kernels")
     ap.add_argument("--gi-async", type=int, default=1, help="overlap the GI update with the previous render")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 collective backend; gloo (host-staged gather, ranks may share a GPU) "
+                         "only rehearses the multi-rank path")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
     args = ap.parse_args()
@@ -94,8 +97,13 @@ def main():
     dist = None
     if world_size > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "gloo":   # rehearsal: ranks may share the GPUs there are
+            local_rank = local_rank % torch.cuda.device_count()
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local_rank)
@@ -150,9 +158,34 @@ def main():
     max_per = (ntiles + world_size - 1) // world_size
     all_ids = [np.arange(q, ntiles, world_size, dtype=np.int32) for q in range(world_size)]
     if world_size > 1:
-        tbuf = torch.empty(max_per * T * T * 4, dtype=torch.uint8, device=dev)
-        r.bind_tile_buffer(tbuf.data_ptr(), tbuf.numel())
-        gather_list = ([torch.empty_like(tbuf) for _ in range(world_size)] if rank == 0 else None)
+        # Double-buffered: frame k's gather (RCCL stream) overlaps frame k+1's
+        # render; rank 0 scatters all ranks' tiles with one rv_untile call.
+        tbufs = [torch.empty(max_per * T * T * 4, dtype=torch.uint8, device=dev) for _ in range(2)]
+        big = ([torch.empty(world_size * max_per * T * T * 4, dtype=torch.uint8, device=dev) for _ in range(2)]
+               if rank == 0 else None)
+        gather_lists = [list(b.chunk(world_size)) for b in big] if rank == 0 else [None, None]
+        cat_ids = np.full(world_size * max_per, -1, dtype=np.int32)   # -1: padding slot
+        for q in range(world_size):
+            cat_ids[q * max_per:q * max_per + len(all_ids[q])] = all_ids[q]
+    pending = []
+    frame_no = [0]
+
+    def issue_gather(b):
+        if args.dist_backend == "nccl":
+            return dist.gather(tbufs[b], gather_lists[b], dst=0, async_op=True)
+        host = tbufs[b].cpu()        # gloo rehearsal: host-staged, synchronous
+        lst = [torch.empty_like(host) for _ in range(world_size)] if rank == 0 else None
+        dist.gather(host, lst, dst=0)
+        if rank == 0:
+            big[b].copy_(torch.cat(lst).to(dev))
+        return None
+
+    def finish():
+        work, b = pending.pop()
+        if work is not None:
+            work.wait()              # the render stream waits for the gather (GPU-side)
+        if rank == 0:
+            r.untile(big[b].data_ptr(), cat_ids, tile_px=T)
 
     def step():
         if cfg.gi_per_frame:
@@ -160,14 +193,22 @@ def main():
         if world_size == 1:
             r.frame(cam, vp, flags=flags)
         else:
+            b = frame_no[0] & 1
+            frame_no[0] += 1
+            r.bind_tile_buffer(tbufs[b].data_ptr(), tbufs[b].numel())
             r.frame_tiles(cam, vp, my_tiles, tile_px=T, flags=flags)
-            dist.gather(tbuf, gather_list, dst=0)
-            if rank == 0:
-                for q in range(world_size):
-                    r.untile(gather_list[q].data_ptr(), all_ids[q], tile_px=T)
+            work = issue_gather(b)
+            if pending:
+                finish()             # frame k-1: gathered while frame k rendered
+            pending.append((work, b))
+
+    def drain():
+        while pending:
+            finish()
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
@@ -175,6 +216,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
@@ -186,16 +228,24 @@ def main():
     r.timing_enable(n_stage_frames)
     for _ in range(n_stage_frames):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     stage_ms, nframes = r.timing_get()
     per_stage_ms, _ = r.timing_stages()
     r.timing_enable(0)
     barrier()
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    gather_check = None
+    if world_size > 1 and rank == 0:   # the gathered frame must equal a one-GPU frame
+        tiled = r.readback(rv.RV_IMAGE_COLOR).copy()
+        r.frame(cam, vp, flags=flags)
+        full = r.readback(rv.RV_IMAGE_COLOR)
+        nbad = int(np.count_nonzero(np.any(tiled != full, axis=-1)))
+        gather_check = "exact" if nbad == 0 else f"{nbad} pixels differ"
     if args.dump and rank == 0:
         write_png(args.dump, r.readback(rv.RV_IMAGE_COLOR))
 
@@ -212,7 +262,8 @@ def main():
     dom = max((k for k in avg_stage_ms if k != "gi"), key=lambda k: avg_stage_ms[k])
     kernel_names = {"pp_primary": "k_prepass" if megakernel else "k_wf_pp_primary",
                     "pp_shadow": "k_wf_pp_shadow",
-                    "primary": "k_render" if megakernel else "k_wf_primary", "shadow": "k_wf_shadow",
+                    "primary": ("k_render_tiles" if world_size > 1 else "k_render") if megakernel else "k_wf_primary",
+                    "shadow": "k_wf_shadow",
                     "water": "k_wf_water", "cones": "k_wf_cones", "shade": "k_wf_shade"}
     dom_ms = avg_stage_ms[dom]
     dom_bytes = stage_bytes[dom]
@@ -221,7 +272,7 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and world_size == 1:   # PMC summaries are of the one-GPU launch
         try:
             tj = json.load(open(tpath))
             if tj.get("kernel", "").startswith(kernel_names[dom]):
@@ -261,6 +312,7 @@ def main():
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
             "path": args.path, "gi_async": bool(args.gi_async),
+            "gather_check": gather_check,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "world_build_s": round(world_s, 3),

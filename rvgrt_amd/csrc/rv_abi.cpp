@@ -15,6 +15,13 @@
 
 using namespace rv;
 
+// Device copy of a host id list, uploaded only when the list changes.
+struct DevIds {
+    int* d = nullptr;
+    size_t cap = 0;
+    std::vector<int32_t> h;
+};
+
 struct rv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -36,7 +43,11 @@ struct rv_ctx {
     float* hdist = nullptr;
     float* hshadow = nullptr;
     unsigned long long* counters = nullptr;
-    int* tile_ids = nullptr; int tile_cap = 0;
+    DevIds tiles;                 // rv_frame_tiles list (device copy, re-uploaded on change)
+    DevIds untile_ids;            // rv_untile list
+    int tiles_px = 0;             // tile size of the cached list
+    std::vector<int> tile_ident;
+    int* tile_order = nullptr; uint32_t* tile_cost = nullptr; size_t tile_ord_cap = 0;   // SCHED_COST per tile slot
     uint32_t* tilebuf = nullptr; size_t tilebuf_bytes = 0;
     uint32_t* ext_tilebuf = nullptr; size_t ext_tilebuf_bytes = 0;
     // stage timing (rv_timing_enable): EV_PER_FRAME events per frame
@@ -224,7 +235,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     }
 #ifdef RV_WAVE_TRACE
     if (getenv("RV_WAVE_TRACE")) {
-        c->wtrace_bytes = (size_t)sched_grid<8>(SCHED_COST, W, H) * 32;   // one 32-B record per wave
+        c->wtrace_bytes = (size_t)sched_grid<8, 8>(SCHED_COST, W, H) * 32;   // one 32-B record per 8x8-pixel wave tile
         if (hipMalloc(&c->wtrace, c->wtrace_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "wave trace");
         hipMemset(c->wtrace, 0, c->wtrace_bytes);
     }
@@ -245,7 +256,8 @@ void rv_destroy(rv_ctx* c) {
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
     hipFree(c->own_color); hipFree(c->own_mv); hipFree(c->own_depth);
     hipFree(c->hdist); hipFree(c->hshadow); hipFree(c->counters);
-    hipFree(c->tile_ids); hipFree(c->tilebuf);
+    hipFree(c->tiles.d); hipFree(c->untile_ids.d); hipFree(c->tile_order); hipFree(c->tile_cost);
+    hipFree(c->tilebuf);
     for (int g = 0; g < 2; g++) { hipFree(c->chunk_order[g]); hipFree(c->chunk_cost[g]); }
     hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
     for (int q = 0; q < NQUEUE; q++) hipFree(c->wq[q]);
@@ -275,6 +287,24 @@ rv_status rv_set_stream(rv_ctx* c, void* s) {
 // side stream waits on this mark before it reads them.
 static rv_status mark_world(rv_ctx* c) {
     HIP_TRY(c, hipEventRecord(c->ev_world, c->stream));
+    return RV_OK;
+}
+
+// Uploads `src` to ids unless it equals the cached list; *changed tells.
+static rv_status upload_ids(rv_ctx* c, DevIds& ids, const int32_t* src, int n, bool* changed) {
+    const bool same = ids.d && ids.h.size() == (size_t)n && (n == 0 || memcmp(ids.h.data(), src, (size_t)n * 4) == 0);
+    if (changed) *changed = !same;
+    if (same) return RV_OK;
+    if ((size_t)n > ids.cap || !ids.d) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        hipFree(ids.d);
+        ids.d = nullptr;
+        ids.cap = 0;
+        HIP_TRY(c, hipMalloc(&ids.d, (size_t)(n > 0 ? n : 1) * 4));
+        ids.cap = (size_t)(n > 0 ? n : 1);
+    }
+    ids.h.assign(src, src + n);   // the copy reads this stable host buffer
+    if (n > 0) HIP_TRY(c, hipMemcpyAsync(ids.d, ids.h.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
     return RV_OK;
 }
 
@@ -527,10 +557,17 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
         // SCHED_COST: re-order the chunks by the wave lifetimes (max over
         // the frames since the last ordering) every order_every frames; a
         // kernel boundary costs ~6 us, the ordering itself ~4 us.
-        if (!tiles && ++c->frames_since_order >= (uint32_t)c->order_every) {
+        if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
             c->frames_since_order = 0;
-            if (pre) launch_chunk_order(c->stream, f, CG_PREPASS, f.hw, f.hh);
-            launch_chunk_order(c->stream, f, CG_RENDER, f.W, f.H);
+            if (tiles) {
+                launch_chunk_order(c->stream, c->tile_cost, c->tile_order, (uint32_t)f.ntiles,
+                                   ((uint32_t)f.ntiles + 7u) & ~7u);
+            } else {
+                if (pre) launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS],
+                                            n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh));
+                launch_chunk_order(c->stream, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER],
+                                   n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H));
+            }
             LAUNCH_CHECK(c);
         }
     } else {
@@ -608,12 +645,6 @@ rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, con
     int tiles_y = (c->cfg.height + tile_px - 1) / tile_px;
     for (int i = 0; i < ntiles; i++)
         if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(c, RV_ERR_INVALID, "tile id out of range");
-    if (ntiles > c->tile_cap) {
-        hipFree(c->tile_ids);
-        c->tile_ids = nullptr;
-        HIP_TRY(c, hipMalloc(&c->tile_ids, (size_t)ntiles * 4));
-        c->tile_cap = ntiles;
-    }
     size_t need = (size_t)ntiles * tile_px * tile_px * 4;
     if (!c->ext_tilebuf && need > c->tilebuf_bytes) {
         hipFree(c->tilebuf);
@@ -621,12 +652,33 @@ rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, con
         HIP_TRY(c, hipMalloc(&c->tilebuf, need));
         c->tilebuf_bytes = need;
     }
-    if (ntiles > 0)
-        HIP_TRY(c, hipMemcpyAsync(c->tile_ids, tile_ids, (size_t)ntiles * 4, hipMemcpyHostToDevice, c->stream));
-    FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
-    f.tiles = c->tile_ids; f.ntiles = ntiles; f.tile_px = tile_px; f.tiles_x = tiles_x;
-    f.tilebuf = c->ext_tilebuf ? c->ext_tilebuf : c->tilebuf;
     if (c->ext_tilebuf && need > c->ext_tilebuf_bytes) return fail(c, RV_ERR_INVALID, "bound tile buffer too small");
+    bool changed = false;
+    rv_status us = upload_ids(c, c->tiles, tile_ids, ntiles, &changed);
+    if (us != RV_OK) return us;
+    if (changed || tile_px != c->tiles_px) {   // new list: identity order, no costs yet
+        const size_t npad = ((size_t)ntiles + 7) & ~(size_t)7;
+        if (npad > c->tile_ord_cap) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            hipFree(c->tile_order); hipFree(c->tile_cost);
+            c->tile_order = nullptr; c->tile_cost = nullptr; c->tile_ord_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->tile_order, npad * 4));
+            HIP_TRY(c, hipMalloc(&c->tile_cost, npad * 4));
+            c->tile_ord_cap = npad;
+        }
+        c->tile_ident.resize(npad);
+        for (size_t i = 0; i < npad; i++) c->tile_ident[i] = (int)i;
+        if (npad) {
+            HIP_TRY(c, hipMemcpyAsync(c->tile_order, c->tile_ident.data(), npad * 4, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemsetAsync(c->tile_cost, 0, npad * 4, c->stream));
+        }
+        c->tiles_px = tile_px;
+        c->frames_since_order = 0;
+    }
+    FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+    f.tiles = c->tiles.d; f.ntiles = ntiles; f.tile_px = tile_px; f.tiles_x = tiles_x;
+    f.tilebuf = c->ext_tilebuf ? c->ext_tilebuf : c->tilebuf;
+    f.chunk_order[CG_RENDER] = c->tile_order; f.chunk_cost[CG_RENDER] = c->tile_cost;
     return run_stages(c, f, true);
 }
 
@@ -694,19 +746,16 @@ rv_status rv_timing_get(rv_ctx* c, double ms[3], int32_t* frames) {
 }
 
 rv_status rv_untile(rv_ctx* c, const void* dev_tiles, const int32_t* tile_ids, int32_t ntiles, int32_t tile_px) {
-    if (!c || (ntiles > 0 && (!dev_tiles || !tile_ids)) || tile_px <= 0) return RV_ERR_INVALID;
+    if (!c || (ntiles > 0 && (!dev_tiles || !tile_ids)) || tile_px <= 0 || ntiles < 0) return RV_ERR_INVALID;
     int tiles_x = (c->cfg.width + tile_px - 1) / tile_px;
     int tiles_y = (c->cfg.height + tile_px - 1) / tile_px;
     for (int i = 0; i < ntiles; i++)
-        if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(c, RV_ERR_INVALID, "tile id out of range");
-    int* ids = nullptr;
-    HIP_TRY(c, hipMallocAsync((void**)&ids, (size_t)(ntiles > 0 ? ntiles : 1) * 4, c->stream));
-    if (ntiles > 0)
-        HIP_TRY(c, hipMemcpyAsync(ids, tile_ids, (size_t)ntiles * 4, hipMemcpyHostToDevice, c->stream));
-    launch_untile(c->stream, (const uint32_t*)dev_tiles, ids, ntiles, tile_px, tiles_x, c->cfg.width,
+        if (tile_ids[i] < -1 || tile_ids[i] >= tiles_x * tiles_y) return fail(c, RV_ERR_INVALID, "tile id out of range");
+    rv_status us = upload_ids(c, c->untile_ids, tile_ids, ntiles, nullptr);
+    if (us != RV_OK) return us;
+    launch_untile(c->stream, (const uint32_t*)dev_tiles, c->untile_ids.d, ntiles, tile_px, tiles_x, c->cfg.width,
                   c->cfg.height, c->color, c->color_pitch);
     LAUNCH_CHECK(c);
-    HIP_TRY(c, hipFreeAsync(ids, c->stream));
     return RV_OK;
 }
 

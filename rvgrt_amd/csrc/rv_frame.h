@@ -51,31 +51,32 @@ __host__ __device__ inline uint32_t chunks_x(uint32_t w) { return (w + CHUNK_PX 
 __host__ __device__ inline uint32_t n_chunks(uint32_t w, uint32_t h) { return chunks_x(w) * chunks_x(h); }
 __host__ __device__ inline uint32_t n_chunks_pad(uint32_t w, uint32_t h) { return (n_chunks(w, h) + 7) & ~7u; }
 
-// Grid of BS x BS-pixel workgroup tiles over a w x h image.
-template <uint32_t BS>
+// Grid of BW x BH-pixel workgroup regions over a w x h image (BW, BH
+// divide CHUNK_PX).
+template <uint32_t BW, uint32_t BH>
 __host__ __device__ inline uint32_t sched_grid(int sched, uint32_t w, uint32_t h) {
-    constexpr uint32_t CBS = CHUNK_PX / BS;
-    if (sched == SCHED_CHUNK || sched == SCHED_COST) return n_chunks_pad(w, h) * CBS * CBS;
-    return ((w + BS - 1) / BS) * ((h + BS - 1) / BS);
+    constexpr uint32_t PER = (CHUNK_PX / BW) * (CHUNK_PX / BH);
+    if (sched == SCHED_CHUNK || sched == SCHED_COST) return n_chunks_pad(w, h) * PER;
+    return ((w + BW - 1) / BW) * ((h + BH - 1) / BH);
 }
 
-// Tile (bx, by) of this workgroup; false for the padding workgroups of a
-// chunked grid and for tiles off the image.
-template <uint32_t BS>
+// Region (bx, by) of this workgroup; false for the padding workgroups of a
+// chunked grid and for regions off the image.
+template <uint32_t BW, uint32_t BH>
 __device__ __forceinline__ bool sched_block(int sched, const int* order, uint32_t w, uint32_t h, uint32_t& bx,
                                             uint32_t& by) {
-    constexpr uint32_t CBS = CHUNK_PX / BS;
-    const uint32_t nbx = (w + BS - 1) / BS, nby = (h + BS - 1) / BS;
+    constexpr uint32_t CX = CHUNK_PX / BW, CY = CHUNK_PX / BH, PER = CX * CY;
+    const uint32_t nbx = (w + BW - 1) / BW, nby = (h + BH - 1) / BH;
     uint32_t b = blockIdx.x;
     if (sched == SCHED_CHUNK || sched == SCHED_COST) {
         // workgroup b runs on XCD b % 8: slot k of that XCD takes sorted chunk
-        // (k / CBS^2) * 8 + xcd, tile k % CBS^2 inside it
+        // (k / PER) * 8 + xcd, region k % PER inside it
         uint32_t xcd = b & 7u, k = b >> 3;
-        uint32_t pos = (k / (CBS * CBS)) * 8 + xcd;
+        uint32_t pos = (k / PER) * 8 + xcd;
         uint32_t chunk = (sched == SCHED_COST && order) ? (uint32_t)order[pos] : pos;
-        uint32_t j = k % (CBS * CBS), ncx = chunks_x(w);
-        bx = (chunk % ncx) * CBS + j % CBS;
-        by = (chunk / ncx) * CBS + j / CBS;
+        uint32_t j = k % PER, ncx = chunks_x(w);
+        bx = (chunk % ncx) * CX + j % CX;
+        by = (chunk / ncx) * CY + j / CX;
         return bx < nbx && by < nby;
     }
     if (sched == SCHED_BAND) b = xcd_swizzle(b, nbx * nby);
@@ -85,11 +86,11 @@ __device__ __forceinline__ bool sched_block(int sched, const int* order, uint32_
 }
 
 // SCHED_COST feedback: every wave reports its lifetime to its chunk.
-template <uint32_t BS>
+template <uint32_t BW, uint32_t BH>
 __device__ __forceinline__ void chunk_cost_report(uint32_t* cost, uint64_t t0, uint32_t w, uint32_t bx, uint32_t by) {
     if (!cost || (threadIdx.x & 63) != 0) return;
     uint64_t dt = wall_clock64() - t0;
-    atomicMax(&cost[(by * BS / CHUNK_PX) * chunks_x(w) + bx * BS / CHUNK_PX],
+    atomicMax(&cost[(by * BH / CHUNK_PX) * chunks_x(w) + bx * BW / CHUNK_PX],
               (uint32_t)(dt > 0xFFFFFFFEull ? 0xFFFFFFFEull : dt) + 1u);
 }
 

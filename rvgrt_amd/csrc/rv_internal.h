@@ -84,8 +84,9 @@ void launch_gi_update(hipStream_t s, const uint32_t* prev, uint32_t* next, const
 uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
-// SCHED_COST: sort the chunk costs of grid g into chunk_order and clear them
-void launch_chunk_order(hipStream_t s, const FrameParams& f, int g, uint32_t w, uint32_t h);
+// SCHED_COST: sort n costs (order has npad >= n entries) into a descending
+// order, clearing the costs
+void launch_chunk_order(hipStream_t s, uint32_t* cost, int* order, uint32_t n, uint32_t npad);
 void launch_prepass_tiles(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render_tiles(hipStream_t s, const World& w, const FrameParams& f);
 // wavefront stages (rv_wavefront.hip); `counters` of f must point at the

@@ -123,7 +123,7 @@ __device__ __forceinline__ bool pixel_of(const FrameParams& f, int W, int H, int
         ix = tx * T + lx; iy = ty * T + ly;
         return lx < T && ly < T && ix < W && iy < H;
     }
-    if (!sched_block<16>(f.sched, nullptr, W, H, bx, by)) { ix = iy = 0; return false; }
+    if (!sched_block<16, 16>(f.sched, nullptr, W, H, bx, by)) { ix = iy = 0; return false; }
     ix = (int)(bx * 16 + (wave & 1) * 8 + (lane & 7));
     iy = (int)(by * 16 + (wave >> 1) * 8 + (lane >> 3));
     return ix < W && iy < H;
@@ -400,7 +400,7 @@ static void launch_queue_kernel(hipStream_t s, K kernel, const World& w, const F
 }
 
 static uint32_t full_grid(const FrameParams& f, int W, int H) {
-    return sched_grid<16>(f.sched, W, H);
+    return sched_grid<16, 16>(f.sched, W, H);
 }
 
 uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles) {
