@@ -165,6 +165,39 @@ def test_frame_tiles_match_full_frame(rv, atlas, flags):
     r.close()
 
 
+@pytest.mark.parametrize("flags", [8, 7])
+def test_cost_ordering_keeps_frames_identical(rv, atlas, flags):
+    """SCHED_COST re-deals chunks/tiles every 4th frame from measured wave
+    lifetimes; the order changes, the pixels must not.  Also: untile skips
+    padding slots (id -1) of a gathered buffer."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H, T = 7, 320, 192, 64
+    r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P1"], W, H)
+    imgs = []
+    for _ in range(9):
+        r.frame(cam, vp)
+        imgs.append(r.readback(rv.RV_IMAGE_COLOR).copy())
+    for im in imgs[1:]:
+        assert np.array_equal(im, imgs[0])
+    tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
+    ids = np.arange(tiles_x * tiles_y, dtype=np.int32)[1::2]
+    sink = rv.StateRender((lg, lg, lg), W, H, flags=flags, atlas=atlas)
+    for k in range(9):
+        r.frame_tiles(cam, vp, ids, tile_px=T)
+        r.sync()
+        p, _ = r.tile_buffer()
+        sink.untile(p, np.concatenate([ids, np.full(3, -1, np.int32)]), tile_px=T)
+        sink.sync()
+        out = sink.readback(rv.RV_IMAGE_COLOR)
+        for t in ids:
+            ty, tx = divmod(int(t), tiles_x)
+            ys, xs = slice(ty * T, min(H, ty * T + T)), slice(tx * T, min(W, tx * T + T))
+            assert np.array_equal(out[ys, xs], imgs[0][ys, xs]), (k, t)
+    sink.close()
+    r.close()
+
+
 def test_draw_cuda_ref_compat(rv, atlas):
     """drawCUDA signature: with ref_compat, time<-jitterY, jitter<-(0, oob)."""
     lg = 6
