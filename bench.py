@@ -78,6 +78,10 @@ def main():
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
     ap.add_argument("--path", default="fused", choices=["fused", "wavefront"],
                     help="frame path: per-pixel megakernels (default) or wavefront stage kernels")
+    ap.add_argument("--stream-priority", type=int, default=-1,
+                    help="torch stream priority of the frame stream (0: the default stream)")
+    ap.add_argument("--gi-per-frame", type=int, default=None,
+                    help="experiments only: override the config's per-frame GI update (0/1)")
     ap.add_argument("--gi-async", type=int, default=1, help="overlap the GI update with the previous render")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collective backend; gloo (host-staged gather, ranks may share a GPU) "
@@ -113,6 +117,7 @@ def main():
             dist.barrier()
 
     cfg = CONFIGS[args.config]
+    gi_per_frame = cfg.gi_per_frame if args.gi_per_frame is None else bool(args.gi_per_frame)
     W, H = cfg.width, cfg.height
     flags = cfg.flags if args.flags is None else args.flags
     prepass = bool(flags & rv.RV_F_PREPASS)
@@ -120,7 +125,11 @@ def main():
 
     # ---------------------------------------------------------------- world
     r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=flags, atlas=atlas, device=local_rank)
-    stream = torch.cuda.current_stream(dev)
+    # the frame stream runs at the highest priority: the library's GI side
+    # stream is created at the lowest, so the GI kernel fills the frame's gaps
+    stream = torch.cuda.Stream(device=dev, priority=args.stream_priority) if args.stream_priority else \
+        torch.cuda.current_stream(dev)
+    torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     r.set_frame_path(args.path)
     r.set_gi_async(args.gi_async)
@@ -188,7 +197,7 @@ def main():
             r.untile(big[b].data_ptr(), cat_ids, tile_px=T)
 
     def step():
-        if cfg.gi_per_frame:
+        if gi_per_frame:
             r.update_gi_data()       # renderLoop: UpdateGIData before drawCUDA
         if world_size == 1:
             r.frame(cam, vp, flags=flags)
@@ -306,9 +315,12 @@ def main():
             "data": "synthetic: procedural world from the reference Evaluate (seed 0), camera pose "
                     f"{args.pose} (reference defaults), random-free",
             "config": {"workload": cfg.name, "world": f"{cfg.n}^3", "resolution": f"{W}x{H}",
-                       "flags": flags, "gi_sweeps": cfg.gi_sweeps, "gi_update_per_frame": cfg.gi_per_frame,
+                       "flags": flags, "gi_sweeps": cfg.gi_sweeps, "gi_update_per_frame": gi_per_frame,
                        "parallelism": f"screen-tiles {T}px x{world_size}" if world_size > 1 else "single-gpu"},
             "rays_per_frame": rays_per_frame,
+            # cone marches are reported separately
+            "cone_steps_per_frame": st_all["cone_steps"],
+            "cone_steps_per_s": round(st_all["cone_steps"] * fps, 1),
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
             "path": args.path, "gi_async": bool(args.gi_async),
@@ -356,7 +368,18 @@ def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
                 done = True
                 break
     dt = time.perf_counter() - t0
+    # the 1-core figure: the same bands on one thread, ~1/4 of the budget
+    O.set_threads(1)
+    t1 = time.perf_counter()
+    rays1 = 0
+    for s in order:
+        rays1 += O.render(w, fr, s, min(H, s + band))["stats"]["traces"]
+        if time.perf_counter() - t1 >= budget_s / 4:
+            break
+    dt1 = time.perf_counter() - t1
+    O.set_threads(threads)
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "value_1core": round(rays1 / dt1 / 1e6, 3),
             "sample": f"oracle/rv_oracle.c render of {rows} rows ({rows / H:.2f} frames) of {cfg.name} in "
                       f"{band}-row bands on {threads} threads ({dt:.1f}s wall, {rays} traces), "
                       "same world/camera/flags"}

@@ -60,6 +60,8 @@ struct rv_ctx {
     // asynchronous GI update (rv_set_gi_async): kernel on gi_stream, copy-back on stream
     bool gi_async = true;
     hipStream_t gi_stream = nullptr;
+    int prio_lo = 0, prio_hi = 0;  // stream priority range (numerically: lo = least urgent)
+    int gi_low_prio = 1;           // RV_GI_PRIO: 1 = GI stream at the lowest priority (fills the frame's gaps)
     hipEvent_t ev_world = nullptr;    // recorded on `stream` after the last world/GI write
     hipEvent_t ev_gi_done = nullptr;  // recorded on gi_stream after a GI kernel
     int enq = 1;                  // RV_WF_ENQ: queue append granularity (FrameParams::enq)
@@ -82,6 +84,8 @@ struct rv_ctx {
 };
 
 namespace {
+
+int gi_prio(const rv_ctx* c) { return c->gi_low_prio ? c->prio_lo : c->prio_hi; }
 
 rv_status fail(rv_ctx* c, rv_status s, const std::string& msg) {
     if (c) c->err = msg;
@@ -206,6 +210,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     hipMemset(c->hdist, 0, hbytes);
     hipMemset(c->hshadow, 0, hbytes);
     if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
+    if (const char* e = getenv("RV_GI_PRIO")) c->gi_low_prio = atoi(e);
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     {   // SCHED_COST chunk order (identity until a frame has been timed) and costs
         const uint32_t nb[2][2] = {{(uint32_t)(W / 2), (uint32_t)(H / 2)}, {(uint32_t)W, (uint32_t)H}};
@@ -242,7 +247,8 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
 #endif
     if (hipEventCreateWithFlags(&c->ev_world, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gi_done, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->gi_stream, hipStreamNonBlocking) != hipSuccess)
+        hipDeviceGetStreamPriorityRange(&c->prio_lo, &c->prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->gi_stream, hipStreamNonBlocking, gi_prio(c)) != hipSuccess)
         return cleanup_fail(RV_ERR_HIP, "gi stream/events");
     if (hipDeviceSynchronize() != hipSuccess) return cleanup_fail(RV_ERR_HIP, "init sync");
     *out = c;
