@@ -29,6 +29,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# Scattered-gather ceiling of the vector L1 / texture path, measured with
+# tools/ubench/gather.hip (profiles/r01_ubench_gather.txt): once a wave's
+# lanes fall in >= 16 lines an L1-resident dword gather costs ~1 cycle per
+# lane per CU -> 256 CUs x 2.4 GHz lane-gathers/s.
+GATHER_CEILING = 256 * 2.4e9
 
 
 def log(*a):
@@ -288,10 +293,20 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    g = st_stage[dom]        # counters of the dominant stage's launch (census frame)
+    gathers = g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]
+    if world_size > 1:
+        gathers = gathers * len(my_tiles) / ntiles
+    gather_rate = gathers / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
     roofline = {"bound": "hbm", "kernel": kernel_names[dom], "achieved": round(achieved, 2),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
-                "avg_launch_ms": round(dom_ms, 4)}
+                "avg_launch_ms": round(dom_ms, 4),
+                # the limit that binds in practice: traversal gathers per second
+                # against the scattered-gather ceiling of the L1/texture path
+                "gathers_per_launch": int(gathers), "gather_rate": round(gather_rate / 1e9, 2),
+                "gather_ceiling": round(GATHER_CEILING / 1e9, 1), "gather_unit": "G lane-gathers/s",
+                "gather_frac": round(gather_rate / GATHER_CEILING, 4)}
 
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
