@@ -73,8 +73,8 @@ def algorithmic_bytes(st: dict, px: int, halfpx: int, prepass: bool, stage: str,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", help="c1..c5 (default c2 = BASELINE configs[1])")
     ap.add_argument("--pose", default="P0")
     ap.add_argument("--tile-px", type=int, default=64)
@@ -91,6 +91,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collective backend; gloo (host-staged gather, ranks may share a GPU) "
                          "only rehearses the multi-rank path")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="frames in flight (default 2 on one GPU, 4 with N>1): frame k renders on stream "
+                         "k %% n with its own frame slot (rv_set_frames_in_flight), so frame k+1 fills frame "
+                         "k's tail; 1 = one frame at a time")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
     args = ap.parse_args()
@@ -137,6 +141,11 @@ def main():
     torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     r.set_frame_path(args.path)
+    nfl = args.inflight if args.inflight is not None else (2 if world_size == 1 else 4)
+    nfl = max(1, nfl if args.path == "fused" else 1)
+    r.set_frames_in_flight(nfl)
+    # frame k is submitted on streams[k % nfl] (streams[0] = the context's stream)
+    streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.stream_priority) for _ in range(nfl - 1)]
     r.set_gi_async(args.gi_async)
     t0 = time.perf_counter()
     r.world_build()
@@ -174,15 +183,17 @@ def main():
     if world_size > 1:
         # Double-buffered: frame k's gather (RCCL stream) overlaps frame k+1's
         # render; rank 0 scatters all ranks' tiles with one rv_untile call.
-        tbufs = [torch.empty(max_per * T * T * 4, dtype=torch.uint8, device=dev) for _ in range(2)]
-        big = ([torch.empty(world_size * max_per * T * T * 4, dtype=torch.uint8, device=dev) for _ in range(2)]
+        nbuf = max(2, nfl)
+        tbufs = [torch.empty(max_per * T * T * 4, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        big = ([torch.empty(world_size * max_per * T * T * 4, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
                if rank == 0 else None)
-        gather_lists = [list(b.chunk(world_size)) for b in big] if rank == 0 else [None, None]
+        gather_lists = [list(b.chunk(world_size)) for b in big] if rank == 0 else [None] * nbuf
         cat_ids = np.full(world_size * max_per, -1, dtype=np.int32)   # -1: padding slot
         for q in range(world_size):
             cat_ids[q * max_per:q * max_per + len(all_ids[q])] = all_ids[q]
     pending = []
     frame_no = [0]
+    serial = [False]        # timing pass: every frame on streams[0]
 
     def issue_gather(b):
         if args.dist_backend == "nccl":
@@ -195,26 +206,37 @@ def main():
         return None
 
     def finish():
-        work, b = pending.pop()
-        if work is not None:
-            work.wait()              # the render stream waits for the gather (GPU-side)
-        if rank == 0:
-            r.untile(big[b].data_ptr(), cat_ids, tile_px=T)
+        work, b, s = pending.pop(0)
+        with torch.cuda.stream(s):
+            if work is not None:
+                work.wait()          # this frame's stream waits for its gather (GPU-side)
+            if rank == 0:
+                r.set_stream(s.cuda_stream)
+                r.untile(big[b].data_ptr(), cat_ids, tile_px=T)
 
     def step():
-        if gi_per_frame:
-            r.update_gi_data()       # renderLoop: UpdateGIData before drawCUDA
+        k = frame_no[0]
+        frame_no[0] += 1
+        s = streams[0] if serial[0] else streams[k % nfl]
         if world_size == 1:
+            r.set_stream(s.cuda_stream)
+            if gi_per_frame:
+                r.update_gi_data()   # renderLoop: UpdateGIData before drawCUDA
             r.frame(cam, vp, flags=flags)
-        else:
-            b = frame_no[0] & 1
-            frame_no[0] += 1
+            return
+        b = k % nbuf
+        with torch.cuda.stream(s):
+            r.set_stream(s.cuda_stream)
+            if gi_per_frame:
+                r.update_gi_data()
             r.bind_tile_buffer(tbufs[b].data_ptr(), tbufs[b].numel())
             r.frame_tiles(cam, vp, my_tiles, tile_px=T, flags=flags)
-            work = issue_gather(b)
-            if pending:
-                finish()             # frame k-1: gathered while frame k rendered
-            pending.append((work, b))
+            work = issue_gather(b)   # the gather waits for this frame's render on stream s
+        pending.append((work, b, s))
+        if nfl == 1 and len(pending) > 1:
+            finish()                 # one frame at a time: untile frame k-1 while k renders
+        elif nfl > 1:
+            finish()                 # frames in flight: untile on the frame's own stream
 
     def drain():
         while pending:
@@ -239,6 +261,7 @@ def main():
     # Per-stage kernel times from HIP events on the context's streams, in a
     # separate pass so the events' own gaps stay out of the timed region.
     n_stage_frames = min(args.steps, 10)
+    serial[0] = True
     r.timing_enable(n_stage_frames)
     for _ in range(n_stage_frames):
         step()
@@ -338,7 +361,7 @@ def main():
             "cone_steps_per_s": round(st_all["cone_steps"] * fps, 1),
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
-            "path": args.path, "gi_async": bool(args.gi_async),
+            "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
             "gather_check": gather_check,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -22,6 +22,23 @@ struct DevIds {
     std::vector<int32_t> h;
 };
 
+// Per-frame resources of one frame in flight (rv_set_frames_in_flight): the
+// library-owned output images, the half-res pre-pass images and the
+// SCHED_COST order/cost arrays.  The active slot's pointers live in rv_ctx's
+// own fields (slot_load/slot_save swap them), so single-slot code paths read
+// exactly what they did before.
+struct FrameSlot {
+    uint32_t* own_color = nullptr; uint32_t* own_mv = nullptr; uint16_t* own_depth = nullptr;
+    float* hdist = nullptr; float* hshadow = nullptr;
+    int* chunk_order[2] = {nullptr, nullptr}; uint32_t* chunk_cost[2] = {nullptr, nullptr};
+    int* tile_order = nullptr; uint32_t* tile_cost = nullptr; size_t tile_ord_cap = 0;
+    int tiles_px = 0; uint32_t frames_since_order = 0;
+    hipEvent_t done = nullptr;    // recorded after the slot's last frame work
+    bool pending = false;         // `done` has been recorded at least once
+    hipStream_t last_stream = nullptr;   // stream of the slot's last frame
+    uint64_t world_seen = 0;      // world version the slot's last frame waited for
+};
+
 struct rv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -80,6 +97,11 @@ struct rv_ctx {
     uint32_t frames_since_order = 0;
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
     uint32_t* chunk_cost[2] = {nullptr, nullptr};
+    std::vector<FrameSlot> slots;  // frames in flight; slots[cur_slot] mirrors the fields above
+    uint64_t world_ver = 1;        // bumped by every world/GI write (mark_world)
+    hipStream_t world_stream = nullptr;   // stream ev_world was recorded on
+    int cur_slot = 0;
+    uint64_t frame_seq = 0;
     std::string err;
 };
 
@@ -103,6 +125,65 @@ rv_status fail(rv_ctx* c, rv_status s, const std::string& msg) {
 #define LAUNCH_CHECK(ctx) HIP_TRY(ctx, hipGetLastError())
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+void slot_save(rv_ctx* c) {
+    FrameSlot& sl = c->slots[c->cur_slot];
+    sl.own_color = c->own_color; sl.own_mv = c->own_mv; sl.own_depth = c->own_depth;
+    sl.hdist = c->hdist; sl.hshadow = c->hshadow;
+    for (int g = 0; g < 2; g++) { sl.chunk_order[g] = c->chunk_order[g]; sl.chunk_cost[g] = c->chunk_cost[g]; }
+    sl.tile_order = c->tile_order; sl.tile_cost = c->tile_cost; sl.tile_ord_cap = c->tile_ord_cap;
+    sl.tiles_px = c->tiles_px; sl.frames_since_order = c->frames_since_order;
+}
+
+void slot_load(rv_ctx* c, int s) {
+    const FrameSlot& sl = c->slots[s];
+    c->cur_slot = s;
+    c->own_color = sl.own_color; c->own_mv = sl.own_mv; c->own_depth = sl.own_depth;
+    if (!c->color_ext) c->color = sl.own_color;
+    if (!c->mv_ext) c->mv = sl.own_mv;
+    if (!c->depth_ext) c->depth = sl.own_depth;
+    c->hdist = sl.hdist; c->hshadow = sl.hshadow;
+    for (int g = 0; g < 2; g++) { c->chunk_order[g] = sl.chunk_order[g]; c->chunk_cost[g] = sl.chunk_cost[g]; }
+    c->tile_order = sl.tile_order; c->tile_cost = sl.tile_cost; c->tile_ord_cap = sl.tile_ord_cap;
+    c->tiles_px = sl.tiles_px; c->frames_since_order = sl.frames_since_order;
+}
+
+// Images (rows padded to 256 B like a D3D12 placed footprint), half-res
+// pre-pass images, identity chunk orders and zero costs of one slot.
+bool slot_alloc(rv_ctx* c, FrameSlot& sl) {
+    const int W = c->cfg.width, H = c->cfg.height;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    if (hipMalloc(&sl.own_color, c->own_color_pitch * H) != hipSuccess ||
+        hipMalloc(&sl.own_mv, c->own_mv_pitch * H) != hipSuccess ||
+        hipMalloc(&sl.own_depth, c->own_depth_pitch * H) != hipSuccess ||
+        hipMalloc(&sl.hdist, hbytes) != hipSuccess || hipMalloc(&sl.hshadow, hbytes) != hipSuccess)
+        return false;
+    hipMemset(sl.own_color, 0, c->own_color_pitch * H);
+    hipMemset(sl.own_mv, 0, c->own_mv_pitch * H);
+    hipMemset(sl.own_depth, 0, c->own_depth_pitch * H);
+    hipMemset(sl.hdist, 0, hbytes);
+    hipMemset(sl.hshadow, 0, hbytes);
+    const uint32_t nb[2][2] = {{(uint32_t)(W / 2), (uint32_t)(H / 2)}, {(uint32_t)W, (uint32_t)H}};
+    for (int g = 0; g < 2; g++) {
+        uint32_t npad = n_chunks_pad(nb[g][0], nb[g][1]);
+        std::vector<int> id(npad);
+        for (uint32_t i = 0; i < npad; i++) id[i] = (int)i;
+        if (hipMalloc(&sl.chunk_order[g], npad * 4) != hipSuccess || hipMalloc(&sl.chunk_cost[g], npad * 4) != hipSuccess)
+            return false;
+        hipMemcpy(sl.chunk_order[g], id.data(), npad * 4, hipMemcpyHostToDevice);
+        hipMemset(sl.chunk_cost[g], 0, npad * 4);
+    }
+    return hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+}
+
+void slot_free(FrameSlot& sl) {
+    hipFree(sl.own_color); hipFree(sl.own_mv); hipFree(sl.own_depth);
+    hipFree(sl.hdist); hipFree(sl.hshadow);
+    for (int g = 0; g < 2; g++) { hipFree(sl.chunk_order[g]); hipFree(sl.chunk_cost[g]); }
+    hipFree(sl.tile_order); hipFree(sl.tile_cost);
+    if (sl.done) hipEventDestroy(sl.done);
+    sl = FrameSlot{};
+}
 
 // per frame: [0, NSTAGE-1) start of each frame stage, [NSTAGE-1] end of the
 // frame, [NSTAGE] / [NSTAGE+1] start / end of the GI update before it
@@ -190,41 +271,18 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
         hipMemcpy(c->atlas, grey.data(), grey.size() * 4, hipMemcpyHostToDevice);
     }
     c->cfg.atlas_rgba8 = nullptr;
-    // frame images, rows padded to 256 B like a D3D12 placed footprint
+    // frame slot 0 (more with rv_set_frames_in_flight)
     int W = cfg->width, H = cfg->height;
     c->own_color_pitch = align256((size_t)W * 4);
     c->own_mv_pitch = align256((size_t)W * 4);
     c->own_depth_pitch = align256((size_t)W * 2);
-    if (hipMalloc(&c->own_color, c->own_color_pitch * H) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "color");
-    if (hipMalloc(&c->own_mv, c->own_mv_pitch * H) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "mv");
-    if (hipMalloc(&c->own_depth, c->own_depth_pitch * H) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "depth");
-    hipMemset(c->own_color, 0, c->own_color_pitch * H);
-    hipMemset(c->own_mv, 0, c->own_mv_pitch * H);
-    hipMemset(c->own_depth, 0, c->own_depth_pitch * H);
-    c->color = c->own_color; c->color_pitch = c->own_color_pitch;
-    c->mv = c->own_mv; c->mv_pitch = c->own_mv_pitch;
-    c->depth = c->own_depth; c->depth_pitch = c->own_depth_pitch;
-    size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
-    if (hipMalloc(&c->hdist, hbytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "halfdist");
-    if (hipMalloc(&c->hshadow, hbytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "halfshadow");
-    hipMemset(c->hdist, 0, hbytes);
-    hipMemset(c->hshadow, 0, hbytes);
+    c->color_pitch = c->own_color_pitch; c->mv_pitch = c->own_mv_pitch; c->depth_pitch = c->own_depth_pitch;
+    c->slots.resize(1);
+    if (!slot_alloc(c, c->slots[0])) return cleanup_fail(RV_ERR_OOM, "frame slot");
+    slot_load(c, 0);
     if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
     if (const char* e = getenv("RV_GI_PRIO")) c->gi_low_prio = atoi(e);
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
-    {   // SCHED_COST chunk order (identity until a frame has been timed) and costs
-        const uint32_t nb[2][2] = {{(uint32_t)(W / 2), (uint32_t)(H / 2)}, {(uint32_t)W, (uint32_t)H}};
-        for (int g = 0; g < 2; g++) {
-            uint32_t npad = n_chunks_pad(nb[g][0], nb[g][1]);
-            std::vector<int> id(npad);
-            for (uint32_t i = 0; i < npad; i++) id[i] = (int)i;
-            if (hipMalloc(&c->chunk_order[g], npad * 4) != hipSuccess ||
-                hipMalloc(&c->chunk_cost[g], npad * 4) != hipSuccess)
-                return cleanup_fail(RV_ERR_OOM, "chunk order");
-            hipMemcpy(c->chunk_order[g], id.data(), npad * 4, hipMemcpyHostToDevice);
-            hipMemset(c->chunk_cost[g], 0, npad * 4);
-        }
-    }
     if (hipMalloc(&c->counters, NSTAGE * NCNT * sizeof(unsigned long long)) != hipSuccess)
         return cleanup_fail(RV_ERR_OOM, "counters");
     hipMemset(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long));
@@ -258,13 +316,13 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
 void rv_destroy(rv_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream); else hipDeviceSynchronize();
+    hipDeviceSynchronize();   // every frame slot's stream
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
-    hipFree(c->own_color); hipFree(c->own_mv); hipFree(c->own_depth);
-    hipFree(c->hdist); hipFree(c->hshadow); hipFree(c->counters);
-    hipFree(c->tiles.d); hipFree(c->untile_ids.d); hipFree(c->tile_order); hipFree(c->tile_cost);
+    if (!c->slots.empty()) slot_save(c);
+    for (FrameSlot& sl : c->slots) slot_free(sl);
+    hipFree(c->counters);
+    hipFree(c->tiles.d); hipFree(c->untile_ids.d);
     hipFree(c->tilebuf);
-    for (int g = 0; g < 2; g++) { hipFree(c->chunk_order[g]); hipFree(c->chunk_cost[g]); }
     hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
     for (int q = 0; q < NQUEUE; q++) hipFree(c->wq[q]);
     for (hipEvent_t e : c->ev) hipEventDestroy(e);
@@ -289,10 +347,52 @@ rv_status rv_set_stream(rv_ctx* c, void* s) {
     return RV_OK;
 }
 
+// Frames in flight: frame k takes slot k % n; its stream first waits for
+// the slot's previous frame (the slot's buffers are reused) and for the last
+// world/GI write (which may have been issued on another stream).
+static rv_status begin_frame(rv_ctx* c) {
+    const int n = (int)c->slots.size();
+    if (n > 1) {
+        const int s = (int)(c->frame_seq % (uint64_t)n);
+        slot_save(c);
+        slot_load(c, s);
+        FrameSlot& sl = c->slots[s];
+        // cross-stream waits only: same-stream work is already ordered
+        if (sl.pending && sl.last_stream != c->stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.done, 0));
+        if (sl.world_seen != c->world_ver || sl.last_stream != c->stream) {
+            if (c->world_stream != c->stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_world, 0));
+            sl.world_seen = c->world_ver;
+        }
+        sl.last_stream = c->stream;
+    }
+    c->frame_seq++;
+    return RV_OK;
+}
+
+static rv_status end_frame(rv_ctx* c) {
+    if (c->slots.size() > 1) {
+        FrameSlot& sl = c->slots[c->cur_slot];
+        HIP_TRY(c, hipEventRecord(sl.done, c->stream));
+        sl.pending = true;
+    }
+    return RV_OK;
+}
+
+// Before anything that rewrites state frames read (world, GI grid, device
+// tile lists): `stream` waits for every frame still in flight.
+static rv_status wait_all_frames(rv_ctx* c) {
+    if (c->slots.size() > 1)
+        for (const FrameSlot& sl : c->slots)
+            if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.done, 0));
+    return RV_OK;
+}
+
 // Everything that writes the world or the GI grid runs on `stream`; the GI
 // side stream waits on this mark before it reads them.
 static rv_status mark_world(rv_ctx* c) {
     HIP_TRY(c, hipEventRecord(c->ev_world, c->stream));
+    c->world_ver++;
+    c->world_stream = c->stream;
     return RV_OK;
 }
 
@@ -301,8 +401,9 @@ static rv_status upload_ids(rv_ctx* c, DevIds& ids, const int32_t* src, int n, b
     const bool same = ids.d && ids.h.size() == (size_t)n && (n == 0 || memcmp(ids.h.data(), src, (size_t)n * 4) == 0);
     if (changed) *changed = !same;
     if (same) return RV_OK;
+    if (rv_status ws = wait_all_frames(c)) return ws;   // frames in flight may read the old list
     if ((size_t)n > ids.cap || !ids.d) {
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, c->slots.size() > 1 ? hipDeviceSynchronize() : hipStreamSynchronize(c->stream));
         hipFree(ids.d);
         ids.d = nullptr;
         ids.cap = 0;
@@ -316,7 +417,29 @@ static rv_status upload_ids(rv_ctx* c, DevIds& ids, const int32_t* src, int n, b
 
 rv_status rv_set_frame_path(rv_ctx* c, int32_t path) {
     if (!c || (path != RV_PATH_FUSED && path != RV_PATH_WAVEFRONT)) return RV_ERR_INVALID;
+    if (path == RV_PATH_WAVEFRONT && c->slots.size() > 1)
+        return fail(c, RV_ERR_STATE, "the wavefront path runs one frame at a time");
     c->megakernel = path == RV_PATH_FUSED;
+    return RV_OK;
+}
+
+rv_status rv_set_frames_in_flight(rv_ctx* c, int32_t n) {
+    if (!c || n < 1 || n > 8) return RV_ERR_INVALID;
+    if (n > 1 && !c->megakernel) return fail(c, RV_ERR_STATE, "frames in flight need the fused path");
+    HIP_TRY(c, hipDeviceSynchronize());
+    slot_save(c);
+    while ((int)c->slots.size() > n) { slot_free(c->slots.back()); c->slots.pop_back(); }
+    while ((int)c->slots.size() < n) {
+        c->slots.emplace_back();
+        if (!slot_alloc(c, c->slots.back())) {
+            slot_free(c->slots.back());
+            c->slots.pop_back();
+            slot_load(c, 0);
+            return fail(c, RV_ERR_OOM, "frame slot");
+        }
+    }
+    slot_load(c, 0);
+    c->frame_seq = 0;
     return RV_OK;
 }
 
@@ -329,11 +452,15 @@ rv_status rv_set_gi_async(rv_ctx* c, int32_t on) {
 rv_status rv_sync(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->slots.size() > 1)
+        for (const FrameSlot& sl : c->slots)
+            if (sl.pending) HIP_TRY(c, hipEventSynchronize(sl.done));
     return RV_OK;
 }
 
 rv_status rv_csdf_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
+    if (rv_status ws = wait_all_frames(c)) return ws;
     uint64_t n = n_csdf(c);
     uint8_t *t0 = nullptr, *t1 = nullptr;
     HIP_TRY(c, hipMallocAsync((void**)&t0, n, c->stream));
@@ -347,6 +474,7 @@ rv_status rv_csdf_build(rv_ctx* c) {
 
 rv_status rv_gi_init(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
+    if (rv_status ws = wait_all_frames(c)) return ws;
     launch_gi_init(c->stream, c->gi, current_world(c), sun_dir(), c->counters + ST_GI * NCNT);
     LAUNCH_CHECK(c);
     c->gi_frame = 0;
@@ -356,6 +484,7 @@ rv_status rv_gi_init(rv_ctx* c) {
 
 rv_status rv_world_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
+    if (rv_status ws = wait_all_frames(c)) return ws;
     launch_fill_bricks(c->stream, c->brick, current_world(c), c->cfg.seed_x, c->cfg.seed_z);
     LAUNCH_CHECK(c);
     rv_status s = rv_csdf_build(c);
@@ -368,6 +497,7 @@ rv_status rv_world_build(rv_ctx* c) {
 
 rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t bytes) {
     if (!c || !host) return RV_ERR_INVALID;
+    if (rv_status ws = wait_all_frames(c)) return ws;
     if (kind == RV_WORLD_BITS) {
         if (bytes != n_bits_words(c) * 4) return fail(c, RV_ERR_INVALID, "bits size mismatch");
         uint32_t* d = nullptr;
@@ -450,6 +580,7 @@ static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t c
         HIP_TRY(c, hipEventRecord(c->ev_gi_done, ks));
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_gi_done, 0));
     }
+    if (rv_status ws = wait_all_frames(c)) return ws;   // frames in flight still read `gi`
     if (count == n) {
         std::swap(c->gi, c->gi_tmp);   // full sweep: flip the double buffer
     } else {
@@ -618,8 +749,10 @@ rv_status rv_frame(rv_ctx* c, const rv_camera* cam, const float* vp16, const flo
                    float jx, float jy, int32_t flags) {
     if (!c || !cam) return RV_ERR_INVALID;
     if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_frame before rv_world_build/import");
+    if (rv_status bs = begin_frame(c)) return bs;
     FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
-    return run_stages(c, f, false);
+    if (rv_status rs = run_stages(c, f, false)) return rs;
+    return end_frame(c);
 }
 
 rv_status rv_draw_cuda(rv_ctx* c, const float pos[3], const float fo[3], const float up[3], const float ri[3],
@@ -659,6 +792,7 @@ rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, con
         c->tilebuf_bytes = need;
     }
     if (c->ext_tilebuf && need > c->ext_tilebuf_bytes) return fail(c, RV_ERR_INVALID, "bound tile buffer too small");
+    if (rv_status bs = begin_frame(c)) return bs;
     bool changed = false;
     rv_status us = upload_ids(c, c->tiles, tile_ids, ntiles, &changed);
     if (us != RV_OK) return us;
@@ -685,7 +819,8 @@ rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, con
     f.tiles = c->tiles.d; f.ntiles = ntiles; f.tile_px = tile_px; f.tiles_x = tiles_x;
     f.tilebuf = c->ext_tilebuf ? c->ext_tilebuf : c->tilebuf;
     f.chunk_order[CG_RENDER] = c->tile_order; f.chunk_cost[CG_RENDER] = c->tile_cost;
-    return run_stages(c, f, true);
+    if (rv_status rs = run_stages(c, f, true)) return rs;
+    return end_frame(c);
 }
 
 rv_status rv_tile_buffer(rv_ctx* c, void** p, size_t* bytes) {
@@ -762,7 +897,7 @@ rv_status rv_untile(rv_ctx* c, const void* dev_tiles, const int32_t* tile_ids, i
     launch_untile(c->stream, (const uint32_t*)dev_tiles, c->untile_ids.d, ntiles, tile_px, tiles_x, c->cfg.width,
                   c->cfg.height, c->color, c->color_pitch);
     LAUNCH_CHECK(c);
-    return RV_OK;
+    return end_frame(c);   // the assembled frame is part of this slot's work
 }
 
 rv_status rv_bind_output(rv_ctx* c, int32_t kind, void* p, size_t pitch) {
@@ -821,6 +956,8 @@ rv_status rv_readback(rv_ctx* c, int32_t kind, void* host, size_t pitch) {
     if (s != RV_OK) return s;
     if (pitch == 0) pitch = rb;
     if (pitch < rb) return fail(c, RV_ERR_INVALID, "host pitch too small");
+    if (c->slots.size() > 1 && c->slots[c->cur_slot].pending)   // the last frame's slot
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->slots[c->cur_slot].done, 0));
     HIP_TRY(c, hipMemcpy2DAsync(host, pitch, p, dp, rb, rows, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return RV_OK;

@@ -19,30 +19,39 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Traversal/shading functions are host+device: the product compiles them
+// for gfx950 only; the CPU test harness (tests/host/) compiles the same
+// source for the host to check this exact code against the oracle.
+#define RV_HD __host__ __device__ __forceinline__
+
 namespace rv {
 
 // ---------------------------------------------------------------- vectors
 struct f3 { float x, y, z; };
-__device__ __forceinline__ f3 V(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
-__device__ __forceinline__ f3 add(f3 a, f3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ f3 sub(f3 a, f3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ f3 mul(f3 a, f3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ f3 scale(f3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ f3 divs(f3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
-__device__ __forceinline__ f3 neg(f3 a) { return V(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
-__device__ __forceinline__ f3 normalize(f3 v) { float l = length(v); return scale(v, 1.0f / l); }
-__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+RV_HD f3 V(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+RV_HD f3 add(f3 a, f3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+RV_HD f3 sub(f3 a, f3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+RV_HD f3 mul(f3 a, f3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+RV_HD f3 scale(f3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+RV_HD f3 divs(f3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+RV_HD f3 neg(f3 a) { return V(-a.x, -a.y, -a.z); }
+RV_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RV_HD float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+RV_HD f3 normalize(f3 v) { float l = length(v); return scale(v, 1.0f / l); }
+RV_HD f3 cross(f3 a, f3 b) {
     return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-__device__ __forceinline__ f3 lerp(f3 a, f3 b, float t) { return add(a, scale(sub(b, a), t)); }
-__device__ __forceinline__ f3 reflect(f3 I, f3 N) { return sub(I, scale(N, 2.0f * dot(I, N))); }
-__device__ __forceinline__ float clampf(float v, float a, float b) { return fmaxf(a, fminf(b, v)); }
+RV_HD f3 lerp(f3 a, f3 b, float t) { return add(a, scale(sub(b, a), t)); }
+RV_HD f3 reflect(f3 I, f3 N) { return sub(I, scale(N, 2.0f * dot(I, N))); }
+RV_HD float clampf(float v, float a, float b) { return fmaxf(a, fminf(b, v)); }
+// explicit-type min/max: the same overload on the host build as on gfx950
+RV_HD uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+RV_HD int imin(int a, int b) { return a < b ? a : b; }
+RV_HD int imax(int a, int b) { return a > b ? a : b; }
 
 // (float)(half)x with round-to-nearest-even (cuda_fp16 __float2half_rn).
-__device__ __forceinline__ float hround(float x) { return (float)(_Float16)x; }
-__device__ __forceinline__ uint16_t hbits(float x) {
+RV_HD float hround(float x) { return (float)(_Float16)x; }
+RV_HD uint16_t hbits(float x) {
     _Float16 h = (_Float16)x; return __builtin_bit_cast(uint16_t, h);
 }
 
@@ -65,6 +74,12 @@ struct World {
 // bits then 64 B of CSDF (coff = 64).  RV_SPLIT_BRICKS=1: a bits region of
 // 64 B per brick followed by a CSDF region of 64 B per brick (coff = 64 x
 // bricks), so a 128-B line covers two bricks of the one a phase reads.
+// DDA look-ahead group (1: one dependent gather per step; 2/4/8: that many
+// cells' words gathered at once, see trace()).
+#ifndef RV_DDA_GROUP
+#define RV_DDA_GROUP 1
+#endif
+
 #ifndef RV_SPLIT_BRICKS
 #define RV_SPLIT_BRICKS 1   // measured: C3 -4 %, C4 -5 % frame time vs one 128-B record
 #endif
@@ -76,66 +91,68 @@ __host__ __device__ inline uint64_t csdf_byte_index(uint32_t coff, uint64_t b, u
     return (uint64_t)coff + (b << BRICK_SHIFT) + local;
 }
 
-__device__ __forceinline__ uint64_t brick_of(const World& w, int bx, int by, int bz) {
+RV_HD uint64_t brick_of(const World& w, int bx, int by, int bz) {
     return (uint64_t)(uint32_t)bx | ((uint64_t)(uint32_t)by << w.lbx) | ((uint64_t)(uint32_t)bz << w.lbxy);
 }
 
 // Byte offset of brick record (bx,by,bz).  The brick array is < 4 GiB
 // (rv_create caps worlds at 2^34 voxels), so offsets stay 32-bit and loads
 // use the SGPR-base + 32-bit VGPR-offset form (no 64-bit address math).
-__device__ __forceinline__ uint32_t brick_byte(const World& w, uint32_t bx, uint32_t by, uint32_t bz) {
+RV_HD uint32_t brick_byte(const World& w, uint32_t bx, uint32_t by, uint32_t bz) {
     return (bx << BRICK_SHIFT) | (by << (w.lbx + BRICK_SHIFT)) | (bz << (w.lbxy + BRICK_SHIFT));
 }
-__device__ __forceinline__ uint32_t load_dword(const World& w, uint32_t byte_off) {
+RV_HD uint32_t load_dword(const World& w, uint32_t byte_off) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + byte_off);
 }
 
 // Bit-word offset of voxel (x,y,z) and the bit inside it: within a brick
 // bit = (x&7) | (y&7)<<3 | (z&7)<<6, dword = bit>>5 = (y>>2 & 1) | (z&7)<<1.
-__device__ __forceinline__ uint32_t voxel_word_off(const World& w, uint32_t x, uint32_t y, uint32_t z) {
+RV_HD uint32_t voxel_word_off(const World& w, uint32_t x, uint32_t y, uint32_t z) {
     return brick_byte(w, x >> 3, y >> 3, z >> 3) | ((y & 4u) << 0) | ((z & 7u) << 3);
 }
-__device__ __forceinline__ uint32_t voxel_bit(uint32_t x, uint32_t y) { return (x & 7u) | ((y & 3u) << 3); }
+RV_HD uint32_t voxel_bit(uint32_t x, uint32_t y) { return (x & 7u) | ((y & 3u) << 3); }
 
 // IsSolid (include/raytracing_functions.cuh:23-26) on the brick layout.
 // Callers pass in-range coordinates (the reference bounds-checks first).
-__device__ __forceinline__ bool is_solid(const World& w, int x, int y, int z) {
+RV_HD bool is_solid(const World& w, int x, int y, int z) {
     uint32_t word = load_dword(w, voxel_word_off(w, (uint32_t)x, (uint32_t)y, (uint32_t)z));
     return (word >> voxel_bit((uint32_t)x, (uint32_t)y)) & 1u;
 }
 
 // CSDF byte of an in-range coarse cell: the dword holding it, then the byte
 // (4x4x4 cells per record, byte = (cx&3) | (cy&3)<<2 | (cz&3)<<4 after 64 B of bits).
-__device__ __forceinline__ uint32_t csdf_at(const World& w, int cx, int cy, int cz) {
-    uint32_t off = (brick_byte(w, (uint32_t)cx >> 2, (uint32_t)cy >> 2, (uint32_t)cz >> 2) + w.coff) |
-                   (((uint32_t)cy & 3u) << 2) | (((uint32_t)cz & 3u) << 4);
-    return (load_dword(w, off) >> (((uint32_t)cx & 3u) << 3)) & 255u;
+RV_HD uint32_t csdf_off(const World& w, uint32_t cx, uint32_t cy, uint32_t cz) {
+    return (brick_byte(w, cx >> 2, cy >> 2, cz >> 2) + w.coff) | ((cy & 3u) << 2) | ((cz & 3u) << 4);
+}
+RV_HD uint32_t csdf_byte(uint32_t word, uint32_t cx) { return (word >> ((cx & 3u) << 3)) & 255u; }
+RV_HD uint32_t csdf_at(const World& w, int cx, int cy, int cz) {
+    return csdf_byte(load_dword(w, csdf_off(w, (uint32_t)cx, (uint32_t)cy, (uint32_t)cz)), (uint32_t)cx);
 }
 
 // getDistance(float3) (include/raytracing_functions.cuh:35-51): truncating
 // cast after floorf*0.5, clamped to the grid (Appendix R11).
-__device__ __forceinline__ float get_distance_f(const World& w, f3 p) {
+RV_HD float get_distance_f(const World& w, f3 p) {
     int cx = (int)(floorf(p.x) * 0.5f);
     int cy = (int)(floorf(p.y) * 0.5f);
     int cz = (int)(floorf(p.z) * 0.5f);
-    cx = max(min(cx, w.SX - 1), 0);
-    cy = max(min(cy, w.SY - 1), 0);
-    cz = max(min(cz, w.SZ - 1), 0);
+    cx = imax(imin(cx, w.SX - 1), 0);
+    cy = imax(imin(cy, w.SY - 1), 0);
+    cz = imax(imin(cz, w.SZ - 1), 0);
     return (float)csdf_at(w, cx, cy, cz);
 }
 
 // getDistance(int3) (include/raytracing_functions.cuh:52-67).
-__device__ __forceinline__ uint32_t get_distance_i(const World& w, int x, int y, int z) {
+RV_HD uint32_t get_distance_i(const World& w, int x, int y, int z) {
     int cx = x / 2, cy = y / 2, cz = z / 2;
-    cx = max(min(cx, w.SX - 1), 0);
-    cy = max(min(cy, w.SY - 1), 0);
-    cz = max(min(cz, w.SZ - 1), 0);
+    cx = imax(imin(cx, w.SX - 1), 0);
+    cy = imax(imin(cy, w.SY - 1), 0);
+    cz = imax(imin(cz, w.SZ - 1), 0);
     return csdf_at(w, cx, cy, cz);
 }
 
 // ---------------------------------------------------------------- noise
 // include/TerrainGeneration.cuh:25-44
-__device__ __forceinline__ uint32_t hash3(int xi, int yi, int zi) {
+RV_HD uint32_t hash3(int xi, int yi, int zi) {
     uint32_t key = (uint32_t)xi * 73856093u;
     key ^= (uint32_t)yi * 19349663u;
     key ^= (uint32_t)zi * 83492791u;
@@ -146,7 +163,7 @@ __device__ __forceinline__ uint32_t hash3(int xi, int yi, int zi) {
     key = key ^ (key >> 15);
     return key;
 }
-__device__ __forceinline__ uint32_t hash2(int xi, int yi) {
+RV_HD uint32_t hash2(int xi, int yi) {
     uint32_t key = (uint32_t)xi * 73856093u;
     key ^= (uint32_t)yi * 19349663u;
     key = (key ^ 61u) ^ (key >> 16);
@@ -158,7 +175,7 @@ __device__ __forceinline__ uint32_t hash2(int xi, int yi) {
 }
 
 // gradient dot product: include/TerrainGeneration.cuh:161-175 + :156-158
-__device__ __forceinline__ float grad_dot3(uint32_t h, float x, float y, float z) {
+RV_HD float grad_dot3(uint32_t h, float x, float y, float z) {
     h &= 15u;
     float gx = (h & 1u) ? 1.0f : -1.0f;
     float gy = (h & 2u) ? 1.0f : -1.0f;
@@ -168,7 +185,7 @@ __device__ __forceinline__ float grad_dot3(uint32_t h, float x, float y, float z
 }
 
 // include/TerrainGeneration.cuh:178-254
-__device__ __forceinline__ float simplex3D(float px, float py, float pz) {
+RV_HD float simplex3D(float px, float py, float pz) {
     const float F3 = 1.0f / 3.0f;
     float s = (px + py + pz) * F3;
     int i = (int)floorf(px + s), j = (int)floorf(py + s), k = (int)floorf(pz + s);
@@ -195,7 +212,7 @@ __device__ __forceinline__ float simplex3D(float px, float py, float pz) {
 }
 
 // include/TerrainGeneration.cuh:65-142 (G2 as written: (3-sqrt3)*0.5)
-__device__ __forceinline__ float simplex2D(float px, float py) {
+RV_HD float simplex2D(float px, float py) {
     const float F2 = (sqrtf(3.0f) - 1.0f) * 0.5f;
     const float G2 = (3.0f - sqrtf(3.0f)) * 0.5f;
     float s = (px + py) * F2;
@@ -223,7 +240,7 @@ __device__ __forceinline__ float simplex2D(float px, float py) {
 }
 
 // include/TerrainGeneration.cuh:259-268
-__device__ __forceinline__ float fbm3D(float x, float y, float z, int oct, float freq, float lac, float pers) {
+RV_HD float fbm3D(float x, float y, float z, int oct, float freq, float lac, float pers) {
     float total = 0.0f, amp = 1.0f;
     for (int i = 0; i < oct; i++) {
         total += simplex3D(x * freq, y * freq, z * freq) * amp;
@@ -234,7 +251,7 @@ __device__ __forceinline__ float fbm3D(float x, float y, float z, int oct, float
 }
 
 // include/TerrainGeneration.cuh:284-356 (float abs on the cave noise: R8)
-__device__ __forceinline__ float evaluate(float x, float y, float z) {
+RV_HD float evaluate(float x, float y, float z) {
     if (y <= 30.0f) return 100.0f;
     float biome = (simplex2D(x * 0.005f, z * 0.005f) + 1.0f) * 0.5f;
     float amp = 60.0f + biome * (400.0f - 60.0f);
@@ -284,7 +301,7 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 //     plus ~20 VALU instructions.
 
 template <bool COUNT>
-__device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
+RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
     H.hit = false; H.undef = false; H.its = 0;
     H.pos = V(-500.0f, -500.0f, -500.0f);
@@ -309,9 +326,9 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
         for (int it = 0; it < 100; it++) {
             int fx = (int)floorf(cur.x), fy = (int)floorf(cur.y), fz = (int)floorf(cur.z);
             oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= Y) | ((uint32_t)fz >= Z);
-            const uint32_t cx = min((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
-            const uint32_t cy = min((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
-            const uint32_t cz = min((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
+            const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
+            const uint32_t cy = umin((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
+            const uint32_t cz = umin((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
             const uint32_t d = csdf_at(w, (int)cx, (int)cy, (int)cz);
             if (COUNT) sc.sphere += !oob;
             const bool stop = oob | (d <= 1);
@@ -330,18 +347,79 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
         mask = -128;
         int st = 0;           // 1: jump, 2: out of bounds, 3: hit
         uint32_t jd = 0;
+#if RV_DDA_GROUP > 1
+        // Look-ahead: the cells a DDA walk visits do not depend on the data
+        // it reads (only where it stops does), so the next G cells' words --
+        // and the CSDF word of an every-8th-step check among them -- are
+        // gathered at once (G independent loads in flight instead of a chain
+        // of G dependent ones), then the G steps are replayed in order on the
+        // loaded words.  Loads past the step where the walk stops are unused.
+        constexpr int G = RV_DDA_GROUP;
+        static_assert(G == 2 || G == 4 || G == 8, "RV_DDA_GROUP divides 8");
+        bool run = true;
+        for (int i0 = 0; i0 < 200 && run; i0 += G) {
+            uint32_t wv[G];
+            uint32_t cw = 0;
+            const bool chk = ((i0 + G - 1) & 7) == 7;   // wave-uniform
+            {
+                int jx = ix, jy = iy, jz = iz;
+                float ux = tx, uy = ty, uz = tz;
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    if (j == G - 1 && chk) {
+                        uint32_t cx = (uint32_t)imin(imax(jx >> 1, 0), w.SX - 1);
+                        uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
+                        uint32_t cz = (uint32_t)imin(imax(jz >> 1, 0), w.SZ - 1);
+                        cw = load_dword(w, csdf_off(w, cx, cy, cz));
+                    }
+                    const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
+                    wv[j] = load_dword(w, voxel_word_off(w, qx, qy, qz));
+                    const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
+                    const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
+                    ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
+                    jx += selx ? sx : 0; jy += sely ? sy : 0; jz += selz ? sz : 0;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < G; j++) {
+                if (j == G - 1 && chk) {
+                    uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
+                    jd = csdf_byte(cw, cx);
+                    if (COUNT) sc.check++;
+                    st = jd > 2 ? 1 : 0;
+                }
+                const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
+                const bool solid = (wv[j] >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
+                if (COUNT) sc.dda += (st == 0) & !oob;
+                st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
+                const bool go = st == 0;
+                const bool cxy = tx < ty, cxz = tx < tz, cyz = ty < tz;
+                const bool selx = go & cxy & cxz;
+                const bool sely = go & !cxy & cyz;
+                const bool selz = go & !(cxy & cxz) & !(!cxy & cyz);
+                tx = selx ? tx + ddx : tx;
+                ty = sely ? ty + ddy : ty;
+                tz = selz ? tz + ddz : tz;
+                ix += selx ? sx : 0;
+                iy += sely ? sy : 0;
+                iz += selz ? sz : 0;
+                mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
+                if (!go) { run = false; break; }
+            }
+        }
+#else
         for (int i = 0; i < 200; i++) {
             if ((i & 7) == 7) {   // i is wave-uniform: a scalar branch
-                uint32_t cx = (uint32_t)min(max(ix >> 1, 0), w.SX - 1);
-                uint32_t cy = (uint32_t)min(max(iy >> 1, 0), w.SY - 1);
-                uint32_t cz = (uint32_t)min(max(iz >> 1, 0), w.SZ - 1);
+                uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
+                uint32_t cy = (uint32_t)imin(imax(iy >> 1, 0), w.SY - 1);
+                uint32_t cz = (uint32_t)imin(imax(iz >> 1, 0), w.SZ - 1);
                 jd = csdf_at(w, (int)cx, (int)cy, (int)cz);
                 if (COUNT) sc.check++;
                 st = jd > 2 ? 1 : 0;
             }
             const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
             // clamped (always valid) gather; its bit only counts in bounds
-            const uint32_t qx = min((uint32_t)ix, X - 1u), qy = min((uint32_t)iy, Y - 1u), qz = min((uint32_t)iz, Z - 1u);
+            const uint32_t qx = umin((uint32_t)ix, X - 1u), qy = umin((uint32_t)iy, Y - 1u), qz = umin((uint32_t)iz, Z - 1u);
             const uint32_t word = load_dword(w, voxel_word_off(w, qx, qy, qz));
             const bool solid = (word >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
             if (COUNT) sc.dda += (st == 0) & !oob;
@@ -360,6 +438,7 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
             mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
             if (!go) break;
         }
+#endif
         if (st == 1) {        // empty space ahead: jump and restart
             f3 c = V((float)ix + 0.5f, (float)iy + 0.5f, (float)iz + 0.5f);
             float t = dot(sub(c, cur), dir);
@@ -401,7 +480,7 @@ __device__ __forceinline__ Hit trace(const World& w, f3 cam, f3 dir, float dist_
 
 // traceCone (src/raytracing_functions.cu:212-273)
 template <bool COUNT>
-__device__ __forceinline__ f3 trace_cone(const World& w, f3 pos, f3 dir, uint32_t& steps) {
+RV_HD f3 trace_cone(const World& w, f3 pos, f3 dir, uint32_t& steps) {
     f3 acc = V(0.0f, 0.0f, 0.0f);
     float alpha = 0.0f;
     float cd = 1.5f * 2.0f;
@@ -430,7 +509,7 @@ __device__ __forceinline__ f3 trace_cone(const World& w, f3 pos, f3 dir, uint32_
 }
 
 // sampleSky (src/raytracing_functions.cu:10-26)
-__device__ __forceinline__ f3 sample_sky(f3 dir, f3 sun) {
+RV_HD f3 sample_sky(f3 dir, f3 sun) {
     if (dot(dir, sun) > 0.999f) return V(1.0f * 10.0f, 0.9f * 10.0f, 0.2f * 10.0f);
     float t = clampf(0.5f * (dir.y + 1.0f), 0.0f, 1.0f);
     return lerp(V(0.2f, 0.4f, 0.8f), V(0.6f, 0.8f, 1.0f), t);
@@ -439,7 +518,7 @@ __device__ __forceinline__ f3 sample_sky(f3 dir, f3 sun) {
 // sampleTexture (src/raytracing_functions.cu:28-62): fp16 UV math, the
 // +121.3 offsets added in double (:43), swapped atlas coords (R10),
 // point filter + wrap on a 256x256 RGBA8 atlas, texel = byte/255.
-__device__ __forceinline__ f3 sample_texture(const World& w, float u, float v, f3 pos) {
+RV_HD f3 sample_texture(const World& w, float u, float v, f3 pos) {
     const float freq = 0.05f;
     float e = simplex3D(floorf(pos.x) * freq, floorf(pos.y) * freq, floorf(pos.z) * freq);
     float e2 = simplex3D(floorf((float)((double)pos.x + 121.3)) * freq * 0.3f,
@@ -460,8 +539,8 @@ __device__ __forceinline__ f3 sample_texture(const World& w, float u, float v, f
     float ux = hround(hround(u * 0.0625f) + bx);
     float uy = hround(hround(v * 0.0625f) + by);
     float cu = uy - floorf(uy), cv = ux - floorf(ux);
-    int col = min((int)floorf(cu * (float)w.aw), w.aw - 1);
-    int row = min((int)floorf(cv * (float)w.ah), w.ah - 1);
+    int col = imin((int)floorf(cu * (float)w.aw), w.aw - 1);
+    int row = imin((int)floorf(cv * (float)w.ah), w.ah - 1);
     uint32_t t = w.atlas[row * w.aw + col];
     return V((float)(t & 255u) / 255.0f, (float)((t >> 8) & 255u) / 255.0f,
              (float)((t >> 16) & 255u) / 255.0f);

@@ -93,6 +93,10 @@ class StateRender:
         p = {"fused": _lib.RV_PATH_FUSED, "wavefront": _lib.RV_PATH_WAVEFRONT}.get(path, path)
         self._check(self._L.rv_set_frame_path(self._h, int(p)), "rv_set_frame_path")
 
+    def set_frames_in_flight(self, n):
+        """Frame slots for concurrent frames on alternating streams (fused path)."""
+        self._check(self._L.rv_set_frames_in_flight(self._h, int(n)), "rv_set_frames_in_flight")
+
     def set_gi_async(self, on):
         self._check(self._L.rv_set_gi_async(self._h, int(bool(on))), "rv_set_gi_async")
 

@@ -1,0 +1,77 @@
+// rv_host_trace.cpp -- TEST INFRASTRUCTURE: the product's traversal source
+// (rvgrt_amd/csrc/rv_device.h, host+device functions) compiled for the CPU,
+// so tests/test_host_trace.py can check that exact code -- including its
+// compile-time variants (RV_DDA_GROUP look-ahead) -- against the oracle on
+// hosts without a GPU.  Not linked into librvgrt_hip.so and not used by it.
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+
+#include "../../rvgrt_amd/csrc/rv_device.h"
+
+using namespace rv;
+
+namespace {
+struct HostWorld {
+    std::vector<uint32_t> brick;
+    World w{};
+};
+
+// Canonical (reference) bits (toIndex order, include/cumath.cuh:33-45) and
+// CSDF (x fastest) -> the product's split brick layout (rv_device.h).
+void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf) {
+    World& w = h.w;
+    w.X = 1 << lx; w.Y = 1 << ly; w.Z = 1 << lz;
+    w.lbx = lx - 3; w.lbxy = (lx - 3) + (ly - 3);
+    w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
+    w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
+    w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
+    const uint64_t nbricks = ((uint64_t)w.X * w.Y * w.Z) / 512;
+    w.coff = csdf_region(nbricks);
+    h.brick.assign((size_t)(((uint64_t)w.X * w.Y * w.Z) / 16), 0u);   // 128 B per brick
+    for (uint64_t z = 0; z < (uint64_t)w.Z; z++)
+        for (uint64_t y = 0; y < (uint64_t)w.Y; y++)
+            for (uint64_t x = 0; x < (uint64_t)w.X; x++) {
+                uint64_t ci = x | (y << lx) | (z << (lx + ly));
+                if (!((bits[ci >> 5] >> (ci & 31)) & 1u)) continue;
+                uint64_t b = (x >> 3) | ((y >> 3) << w.lbx) | ((z >> 3) << w.lbxy);
+                uint32_t bit = (uint32_t)((x & 7) | ((y & 7) << 3) | ((z & 7) << 6));
+                h.brick[bits_word_index(b, bit >> 5)] |= 1u << (bit & 31);
+            }
+    uint8_t* bytes = reinterpret_cast<uint8_t*>(h.brick.data());
+    for (uint64_t cz = 0; cz < (uint64_t)w.SZ; cz++)
+        for (uint64_t cy = 0; cy < (uint64_t)w.SY; cy++)
+            for (uint64_t cx = 0; cx < (uint64_t)w.SX; cx++) {
+                uint64_t b = (cx >> 2) | ((cy >> 2) << w.lbx) | ((cz >> 2) << w.lbxy);
+                uint32_t local = (uint32_t)((cx & 3) | ((cy & 3) << 2) | ((cz & 3) << 4));
+                bytes[csdf_byte_index(w.coff, b, local)] = csdf[(cz * w.SY + cy) * w.SX + cx];
+            }
+    w.brick = h.brick.data();
+}
+}  // namespace
+
+extern "C" {
+
+// Out record per ray (48 B): pos[3], normal[3], u, v, hit, undef, sphere, dda, check (ints)
+struct HostHit { float pos[3], normal[3], u, v; int32_t hit, undef, sphere, dda, check, pad; };
+
+int rvh_dda_group(void) { return RV_DDA_GROUP; }
+
+int rvh_trace_rays(int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
+                   const float* dir, const float* dist, int64_t n, HostHit* out) {
+    HostWorld h;
+    build(h, lx, ly, lz, bits, csdf);
+    for (int64_t i = 0; i < n; i++) {
+        StepCount sc{};
+        Hit r = trace<true>(h.w, V(org[3 * i], org[3 * i + 1], org[3 * i + 2]),
+                            V(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), hround(dist[i]), sc);
+        HostHit& o = out[i];
+        o.pos[0] = r.pos.x; o.pos[1] = r.pos.y; o.pos[2] = r.pos.z;
+        o.normal[0] = r.normal.x; o.normal[1] = r.normal.y; o.normal[2] = r.normal.z;
+        o.u = r.u; o.v = r.v; o.hit = r.hit; o.undef = r.undef;
+        o.sphere = (int)sc.sphere; o.dda = (int)sc.dda; o.check = (int)sc.check; o.pad = 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -298,3 +298,86 @@ def test_gi_async_update_matches_serial_and_oracle(rv, atlas, oracle_world):
         ow.gi_update(k, first=off, count=min(rays, n - off))
         off = 0 if off + rays >= n else off + rays
     assert np.array_equal(res[1][0], ow.gi)
+
+
+class _Hip:
+    """Streams and device buffers from the HIP runtime the library loaded
+    (the test must not bring in a second runtime through torch)."""
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.L = C.CDLL("libamdhip64.so.7")
+        self.owned = []
+
+    def stream(self):
+        s = self.C.c_void_p()
+        assert self.L.hipStreamCreate(self.C.byref(s)) == 0
+        self.owned.append(("s", s))
+        return s.value
+
+    def malloc(self, n):
+        p = self.C.c_void_p()
+        assert self.L.hipMalloc(self.C.byref(p), self.C.c_size_t(n)) == 0
+        assert self.L.hipMemset(p, 0, self.C.c_size_t(n)) == 0
+        self.owned.append(("m", p))
+        return p.value
+
+    def close(self):
+        self.L.hipDeviceSynchronize()
+        for kind, h in self.owned:
+            (self.L.hipStreamDestroy if kind == "s" else self.L.hipFree)(h)
+
+
+@pytest.mark.parametrize("flags", [8, 7])
+def test_frames_in_flight_identical(rv, atlas, flags):
+    """rv_set_frames_in_flight: frames submitted on alternating streams, each
+    in its own frame slot (images, half-res images, scheduling state), render
+    concurrently and equal the one-at-a-time frame in colour, MV and depth;
+    per-frame GI updates (flags 7) wait for the frames in flight.  Also the
+    tile path with one tile buffer per slot."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H, T = 7, 320, 192, 64
+    hip = _Hip()
+    ref = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
+    r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    r.set_frames_in_flight(3)
+    streams = [hip.stream() for _ in range(3)]
+    gi = bool(flags & rv.RV_F_GI)
+    kinds = (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH)
+    for k in range(7):
+        if gi:
+            ref.update_gi_data()
+        ref.frame(cam, vp)
+        want = [ref.readback(kind).copy() for kind in kinds]
+        r.set_stream(streams[k % 3])
+        if gi:
+            r.update_gi_data()
+        r.frame(cam, vp)
+        if k % 2 == 0:   # read back some frames while others are in flight
+            for kind, b in zip(kinds, want):
+                assert np.array_equal(r.readback(kind), b), (k, kind)
+    r.sync()
+    if not gi:   # tiles: three slots, three tile buffers, untiled into a sink
+        tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
+        ids = np.arange(tiles_x * tiles_y, dtype=np.int32)
+        nbytes = len(ids) * T * T * 4
+        bufs = [hip.malloc(nbytes) for _ in range(3)]
+        sink = rv.StateRender((lg, lg, lg), W, H, flags=flags, atlas=atlas)
+        for k in range(6):
+            r.set_stream(streams[k % 3])
+            r.bind_tile_buffer(bufs[k % 3], nbytes)
+            r.frame_tiles(cam, vp, ids, tile_px=T)
+        r.sync()
+        for k in range(3):
+            sink.untile(bufs[k], ids, tile_px=T)
+            sink.sync()
+            assert np.array_equal(sink.readback(rv.RV_IMAGE_COLOR), want[0]), k
+        sink.close()
+    with pytest.raises(rv.RvError):
+        r.set_frame_path("wavefront")   # one frame at a time only
+    r.set_frames_in_flight(1)
+    r.set_stream(0)
+    r.close()
+    ref.close()
+    hip.close()

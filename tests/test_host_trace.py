@@ -1,0 +1,60 @@
+"""The product's traversal source (rvgrt_amd/csrc/rv_device.h) compiled for
+the CPU (tests/host/rv_host_trace.cpp) against the oracle: hit, position,
+normal, uv and sphere/DDA/check step counts bit-exact on random rays, for
+every DDA look-ahead group size the GPU build can select (RV_DDA_GROUP).
+Runs without a GPU; the GPU build of the same source is checked by
+tests/test_gpu_parity.py::test_trace_bit_exact."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import random_rays
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HOST = os.path.join(HERE, "host")
+HIT = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("u", "<f4"), ("v", "<f4"), ("hit", "<i4"),
+                ("undef", "<i4"), ("sphere", "<i4"), ("dda", "<i4"), ("check", "<i4"), ("pad", "<i4")])
+
+
+@pytest.fixture(scope="module")
+def host_libs():
+    subprocess.run(["make", "-s", "-C", HOST], check=True)
+    libs = {}
+    for g in (1, 2, 4, 8):
+        L = C.CDLL(os.path.join(HOST, "build", f"librvhost_g{g}.so"))
+        L.rvh_trace_rays.restype = C.c_int
+        L.rvh_trace_rays.argtypes = [C.c_int] * 3 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p]
+        assert L.rvh_dda_group() == g
+        libs[g] = L
+    return libs
+
+
+def _trace(L, ow, org, d, dist):
+    out = np.zeros(len(dist), HIT)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    assert L.rvh_trace_rays(ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(org), p(d), p(dist),
+                            len(dist), p(out)) == 0
+    return out
+
+
+@pytest.mark.parametrize("dims", [(7, 7, 7), (8, 6, 7)])
+@pytest.mark.parametrize("group", [1, 2, 4, 8])
+def test_host_trace_bit_exact(host_libs, oracle_world, dims, group):
+    ow = oracle_world(*dims, gi_sweeps=0)
+    rng = np.random.default_rng(4321)
+    org, d, dist = random_rays(rng, 20000, (ow.X, ow.Y, ow.Z))
+    g = _trace(host_libs[group], ow, org, d, dist)
+    o = ow.trace_batch(org, d, dist)
+    assert (g["hit"] == o["hit"]).all()
+    assert (g["undef"] == o["undef"]).all()
+    assert np.array_equal(g["pos"].view(np.uint32), o["pos"].view(np.uint32))
+    assert np.array_equal(g["normal"], o["normal"])
+    assert np.array_equal(g["u"].view(np.uint32), o["u"].view(np.uint32))
+    assert np.array_equal(g["v"].view(np.uint32), o["v"].view(np.uint32))
+    assert np.array_equal(g["sphere"], o["n_sphere"])
+    assert np.array_equal(g["dda"], o["n_dda"])
+    assert np.array_equal(g["check"], o["n_check"])
+    assert g["hit"].mean() > 0.2 and (g["dda"] > 100).any()
