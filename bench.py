@@ -95,6 +95,9 @@ def main():
                     help="frames in flight (default 2 on one GPU, 4 with N>1): frame k renders on stream "
                          "k %% n with its own frame slot (rv_set_frames_in_flight), so frame k+1 fills frame "
                          "k's tail; 1 = one frame at a time")
+    ap.add_argument("--loop", default="native", choices=["native", "python"],
+                    help="frame loop: rv_render_frames (C++: slots, streams, RCCL gather, untile) or the "
+                         "per-frame Python loop over the same library calls (torch.distributed gather)")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
     args = ap.parse_args()
@@ -194,6 +197,20 @@ def main():
     pending = []
     frame_no = [0]
     serial = [False]        # timing pass: every frame on streams[0]
+    native = args.loop == "native" and (world_size == 1 or args.dist_backend == "nccl")
+    comm = None
+    if native and world_size > 1:
+        # RCCL communicator of the library (joins torch's librccl); id from rank 0
+        r.set_tile_shard(T, rank, world_size)
+        uid = torch.zeros(rv.Comm.ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            uid.copy_(torch.tensor(list(rv.Comm.unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        comm = rv.Comm(r, bytes(uid.cpu().tolist()), world_size, rank)
+
+    def run_native(k):
+        r.set_stream(stream.cuda_stream)
+        r.render_frames(k, cam, vp, flags=flags, gi_per_frame=gi_per_frame, comm=comm)
 
     def issue_gather(b):
         if args.dist_backend == "nccl":
@@ -242,17 +259,23 @@ def main():
         while pending:
             finish()
 
-    for _ in range(args.warmup):
-        step()
-    drain()
+    if native:
+        run_native(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            step()
+        drain()
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
 
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
+    if native:
+        run_native(args.steps)
+    else:
+        for _ in range(args.steps):
+            step()
+        drain()
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
@@ -263,9 +286,14 @@ def main():
     n_stage_frames = min(args.steps, 10)
     serial[0] = True
     r.timing_enable(n_stage_frames)
-    for _ in range(n_stage_frames):
-        step()
-    drain()
+    if native:   # one frame at a time on the context's stream (rv_render_frames, 1 slot in use)
+        r.set_frames_in_flight(1)
+        run_native(n_stage_frames)
+        r.set_frames_in_flight(nfl)
+    else:
+        for _ in range(n_stage_frames):
+            step()
+        drain()
     torch.cuda.synchronize(dev)
     stage_ms, nframes = r.timing_get()
     per_stage_ms, _ = r.timing_stages()
@@ -362,6 +390,8 @@ def main():
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
+            "loop": "native" if native else "python",
+            "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,
             "gather_check": gather_check,
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -369,6 +399,8 @@ def main():
             "stats": st_all,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     r.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -1,7 +1,9 @@
 // rv_abi.cpp -- host side of librvgrt_hip.so: the C ABI declared in
 // include/rvgrt.h.  Owns device memory, the HIP stream and the GI update
 // state; every entry point converts failures into rv_status + message.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: RCCL is resolved at run time (rccl_load)
 
 #include <chrono>
 #include <cmath>
@@ -36,7 +38,12 @@ struct FrameSlot {
     hipEvent_t done = nullptr;    // recorded after the slot's last frame work
     bool pending = false;         // `done` has been recorded at least once
     hipStream_t last_stream = nullptr;   // stream of the slot's last frame
+    uint64_t submitted = 0;       // frame_seq of the slot's last frame
     uint64_t world_seen = 0;      // world version the slot's last frame waited for
+    // rv_render_frames with a tile shard: packed tiles, rank-0 gather buffer
+    uint32_t* tbuf = nullptr; size_t tbytes = 0;
+    uint32_t* gbuf = nullptr; size_t gbytes = 0;
+    hipEvent_t gathered = nullptr;      // recorded on the comm stream after the slot's gather
 };
 
 struct rv_ctx {
@@ -98,7 +105,15 @@ struct rv_ctx {
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
     uint32_t* chunk_cost[2] = {nullptr, nullptr};
     std::vector<FrameSlot> slots;  // frames in flight; slots[cur_slot] mirrors the fields above
+    std::vector<hipStream_t> fstreams;   // rv_render_frames: streams of slots 1..n-1 (slot 0: `stream`)
+    int fstream_prio = 0;
+    hipStream_t comm_stream = nullptr;   // rv_render_frames: RCCL gathers, in frame order
+    hipEvent_t ev_loop = nullptr;        // scratch event of rv_render_frames
+    // rv_set_tile_shard: this rank's tiles and the gathered layout (rank 0)
+    int shard_px = 0, shard_rank = 0, shard_n = 0, shard_max = 0;
+    std::vector<int32_t> shard_ids, shard_all;
     uint64_t world_ver = 1;        // bumped by every world/GI write (mark_world)
+    uint64_t gi_swapped_at = 0;    // frame_seq at the last GI buffer flip: older frames read gi_tmp
     hipStream_t world_stream = nullptr;   // stream ev_world was recorded on
     int cur_slot = 0;
     uint64_t frame_seq = 0;
@@ -173,7 +188,8 @@ bool slot_alloc(rv_ctx* c, FrameSlot& sl) {
         hipMemcpy(sl.chunk_order[g], id.data(), npad * 4, hipMemcpyHostToDevice);
         hipMemset(sl.chunk_cost[g], 0, npad * 4);
     }
-    return hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+    return hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&sl.gathered, hipEventDisableTiming) == hipSuccess;
 }
 
 void slot_free(FrameSlot& sl) {
@@ -181,7 +197,9 @@ void slot_free(FrameSlot& sl) {
     hipFree(sl.hdist); hipFree(sl.hshadow);
     for (int g = 0; g < 2; g++) { hipFree(sl.chunk_order[g]); hipFree(sl.chunk_cost[g]); }
     hipFree(sl.tile_order); hipFree(sl.tile_cost);
+    hipFree(sl.tbuf); hipFree(sl.gbuf);
     if (sl.done) hipEventDestroy(sl.done);
+    if (sl.gathered) hipEventDestroy(sl.gathered);
     sl = FrameSlot{};
 }
 
@@ -336,6 +354,9 @@ void rv_destroy(rv_ctx* c) {
     }
 #endif
     if (c->gi_stream) { hipStreamSynchronize(c->gi_stream); hipStreamDestroy(c->gi_stream); }
+    for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
+    if (c->comm_stream) hipStreamDestroy(c->comm_stream);
+    if (c->ev_loop) hipEventDestroy(c->ev_loop);
     if (c->ev_world) hipEventDestroy(c->ev_world);
     if (c->ev_gi_done) hipEventDestroy(c->ev_gi_done);
     delete c;
@@ -364,6 +385,7 @@ static rv_status begin_frame(rv_ctx* c) {
             sl.world_seen = c->world_ver;
         }
         sl.last_stream = c->stream;
+        sl.submitted = c->frame_seq;
     }
     c->frame_seq++;
     return RV_OK;
@@ -381,6 +403,7 @@ static rv_status end_frame(rv_ctx* c) {
 // Before anything that rewrites state frames read (world, GI grid, device
 // tile lists): `stream` waits for every frame still in flight.
 static rv_status wait_all_frames(rv_ctx* c) {
+    if (c->world_stream != c->stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_world, 0));   // write after write
     if (c->slots.size() > 1)
         for (const FrameSlot& sl : c->slots)
             if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.done, 0));
@@ -570,7 +593,13 @@ static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t c
     if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
     if (count == n) async = false;   // full sweep flips the double buffer instead
     hipStream_t ks = async ? c->gi_stream : c->stream;
-    if (async) HIP_TRY(c, hipStreamWaitEvent(ks, c->ev_world, 0));
+    // the last world/GI write may have been issued on another stream
+    if (async || c->world_stream != ks) HIP_TRY(c, hipStreamWaitEvent(ks, c->ev_world, 0));
+    // gi_tmp is about to be written: frames in flight from before the last
+    // flip of the double buffer still read it
+    if (c->slots.size() > 1)
+        for (const FrameSlot& sl : c->slots)
+            if (sl.pending && sl.submitted < c->gi_swapped_at) HIP_TRY(c, hipStreamWaitEvent(ks, sl.done, 0));
     if (t0) HIP_TRY(c, hipEventRecord(t0, ks));
     launch_gi_update(ks, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count,
                      c->counters + ST_GI * NCNT);
@@ -583,6 +612,7 @@ static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t c
     if (rv_status ws = wait_all_frames(c)) return ws;   // frames in flight still read `gi`
     if (count == n) {
         std::swap(c->gi, c->gi_tmp);   // full sweep: flip the double buffer
+        c->gi_swapped_at = c->frame_seq;
     } else {
         HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice,
                                   c->stream));
@@ -1063,6 +1093,217 @@ rv_status rv_stats_get(rv_ctx* c, rv_stats* out) { return rv_stats_stage(c, -1, 
 rv_status rv_stats_reset(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long), c->stream));
+    return RV_OK;
+}
+
+}  // extern "C"
+
+// ===================================================================== render loop
+// RCCL, resolved at run time from the library the process already uses
+// (torch's bundled librccl when called from Python: pass its path), so no
+// second RCCL/HIP runtime is loaded next to it.
+namespace {
+struct RcclApi {
+    void* h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+RcclApi g_rccl;
+
+bool rccl_load(const char* path, std::string& err) {
+    if (g_rccl.h) return true;
+    const char* names[] = {path, "librccl.so.1", "librccl.so"};
+    for (const char* n : names) {
+        if (!n || !*n) continue;
+        g_rccl.h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+        if (g_rccl.h) break;
+    }
+    if (!g_rccl.h) { err = std::string("dlopen librccl: ") + dlerror(); return false; }
+    auto sym = [&](const char* n) { return dlsym(g_rccl.h, n); };
+    g_rccl.get_unique_id = (decltype(g_rccl.get_unique_id))sym("ncclGetUniqueId");
+    g_rccl.comm_init_rank = (decltype(g_rccl.comm_init_rank))sym("ncclCommInitRank");
+    g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))sym("ncclCommDestroy");
+    g_rccl.send = (decltype(g_rccl.send))sym("ncclSend");
+    g_rccl.recv = (decltype(g_rccl.recv))sym("ncclRecv");
+    g_rccl.group_start = (decltype(g_rccl.group_start))sym("ncclGroupStart");
+    g_rccl.group_end = (decltype(g_rccl.group_end))sym("ncclGroupEnd");
+    g_rccl.error_string = (decltype(g_rccl.error_string))sym("ncclGetErrorString");
+    if (!g_rccl.get_unique_id || !g_rccl.comm_init_rank || !g_rccl.comm_destroy || !g_rccl.send || !g_rccl.recv ||
+        !g_rccl.group_start || !g_rccl.group_end || !g_rccl.error_string) {
+        err = "librccl lacks a required symbol";
+        g_rccl = RcclApi{};
+        return false;
+    }
+    return true;
+}
+}  // namespace
+
+struct rv_comm {
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1, device = 0;
+};
+
+#define NCCL_TRY(ctx, expr)                                                                  \
+    do {                                                                                     \
+        ncclResult_t r_ = (expr);                                                            \
+        if (r_ != ncclSuccess)                                                               \
+            return fail((ctx), RV_ERR_HIP, std::string(#expr) + ": " + g_rccl.error_string(r_)); \
+    } while (0)
+
+extern "C" {
+
+rv_status rv_comm_unique_id(const char* rccl_path, void* id, size_t bytes) {
+    if (!id || bytes < sizeof(ncclUniqueId)) return RV_ERR_INVALID;
+    std::string err;
+    if (!rccl_load(rccl_path, err)) return RV_ERR_HIP;
+    ncclUniqueId u;
+    if (g_rccl.get_unique_id(&u) != ncclSuccess) return RV_ERR_HIP;
+    memcpy(id, &u, sizeof(u));
+    return RV_OK;
+}
+
+rv_status rv_comm_create(rv_ctx* c, const char* rccl_path, const void* id, size_t bytes, int32_t nranks, int32_t rank,
+                         rv_comm** out) {
+    if (!c || !id || !out || bytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
+        return RV_ERR_INVALID;
+    *out = nullptr;
+    std::string err;
+    if (!rccl_load(rccl_path, err)) return fail(c, RV_ERR_HIP, err);
+    HIP_TRY(c, hipSetDevice(c->device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    rv_comm* m = new rv_comm();
+    m->rank = rank; m->nranks = nranks; m->device = c->device;
+    ncclResult_t r = g_rccl.comm_init_rank(&m->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete m;
+        return fail(c, RV_ERR_HIP, std::string("ncclCommInitRank: ") + g_rccl.error_string(r));
+    }
+    *out = m;
+    return RV_OK;
+}
+
+void rv_comm_destroy(rv_comm* m) {
+    if (!m) return;
+    if (m->comm && g_rccl.comm_destroy) {
+        hipSetDevice(m->device);
+        hipDeviceSynchronize();
+        g_rccl.comm_destroy(m->comm);
+    }
+    delete m;
+}
+
+rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks) {
+    if (!c || nranks < 0 || (nranks > 0 && (rank < 0 || rank >= nranks))) return RV_ERR_INVALID;
+    if (nranks > 0 && (tile_px < 16 || (tile_px & 15))) return fail(c, RV_ERR_INVALID, "tile_px must be a multiple of 16");
+    c->shard_n = nranks; c->shard_rank = rank; c->shard_px = tile_px;
+    c->shard_ids.clear(); c->shard_all.clear(); c->shard_max = 0;
+    if (nranks == 0) return RV_OK;
+    const int tx = (c->cfg.width + tile_px - 1) / tile_px, ty = (c->cfg.height + tile_px - 1) / tile_px;
+    const int nt = tx * ty;
+    c->shard_max = (nt + nranks - 1) / nranks;
+    for (int t = rank; t < nt; t += nranks) c->shard_ids.push_back(t);   // interleaved (tiles.py rank_tiles)
+    c->shard_all.assign((size_t)nranks * c->shard_max, -1);              // gathered layout, -1 = padding slot
+    for (int q = 0; q < nranks; q++) {
+        int k = 0;
+        for (int t = q; t < nt; t += nranks) c->shard_all[(size_t)q * c->shard_max + k++] = t;
+    }
+    return RV_OK;
+}
+
+rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16, const float* pvp16,
+                           float time, float jx, float jy, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
+    if (!c || !cam || frames < 0) return RV_ERR_INVALID;
+    if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_render_frames before world");
+    if (comm && (c->shard_n != comm->nranks || c->shard_rank != comm->rank))
+        return fail(c, RV_ERR_INVALID, "tile shard does not match the communicator");
+    const int n = (int)c->slots.size();
+    const bool tiles = c->shard_n > 0;
+    const int T = c->shard_px;
+    const size_t slice = (size_t)c->shard_max * T * T * 4;
+    // streams of slots 1..n-1, the comm stream and buffers, created on first use
+    int prio = 0;   // slot streams run at the caller stream's priority
+    if (c->stream) HIP_TRY(c, hipStreamGetPriority(c->stream, &prio));
+    if (!c->fstreams.empty() && c->fstream_prio != prio) {
+        HIP_TRY(c, hipDeviceSynchronize());
+        for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
+        c->fstreams.clear();
+    }
+    c->fstream_prio = prio;
+    while ((int)c->fstreams.size() < n - 1) {
+        hipStream_t st;
+        HIP_TRY(c, hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
+        c->fstreams.push_back(st);
+    }
+    if (!c->ev_loop) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_loop, hipEventDisableTiming));
+    if (tiles) {
+        if (comm && !c->comm_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        const bool root = c->shard_rank == 0;
+        const size_t gneed = root ? slice * (size_t)c->shard_n : 0;
+        for (FrameSlot& sl : c->slots) {
+            if (sl.tbytes != slice || sl.gbytes != gneed) {
+                HIP_TRY(c, hipDeviceSynchronize());
+                hipFree(sl.tbuf); hipFree(sl.gbuf);
+                sl.tbuf = nullptr; sl.gbuf = nullptr; sl.tbytes = sl.gbytes = 0;
+                HIP_TRY(c, hipMalloc(&sl.tbuf, slice));
+                if (gneed) HIP_TRY(c, hipMalloc(&sl.gbuf, gneed));
+                sl.tbytes = slice; sl.gbytes = gneed;
+            }
+        }
+    }
+    hipStream_t caller = c->stream;
+    uint32_t* saved_ext = c->ext_tilebuf; size_t saved_ext_bytes = c->ext_tilebuf_bytes;
+    rv_status st = RV_OK;
+    // the loop's streams start after the caller's work so far
+    HIP_TRY(c, hipEventRecord(c->ev_loop, caller));
+    for (hipStream_t fs : c->fstreams) HIP_TRY(c, hipStreamWaitEvent(fs, c->ev_loop, 0));
+    if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_loop, 0));
+    for (int k = 0; k < frames && st == RV_OK; k++) {
+        const int s = (int)(c->frame_seq % (uint64_t)n);   // the slot begin_frame will pick
+        c->stream = s == 0 ? caller : c->fstreams[s - 1];
+        if (gi_per_frame && (st = rv_update_gi_data(c)) != RV_OK) break;
+        if (!tiles) { st = rv_frame(c, cam, vp16, pvp16, time, jx, jy, flags); continue; }
+        FrameSlot& sl = c->slots[s];
+        c->ext_tilebuf = sl.tbuf; c->ext_tilebuf_bytes = sl.tbytes;
+        st = rv_frame_tiles(c, cam, vp16, pvp16, time, jx, jy, flags, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T);
+        if (st != RV_OK) break;
+        HIP_TRY(c, hipEventRecord(sl.done, c->stream));   // the render, also with one slot
+        sl.pending = true;
+        if (comm) {   // gather to rank 0 on the comm stream, in frame order on every rank
+            HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, sl.done, 0));
+            if (c->shard_rank == 0)
+                HIP_TRY(c, hipMemcpyAsync(sl.gbuf, sl.tbuf, slice, hipMemcpyDeviceToDevice, c->comm_stream));
+            NCCL_TRY(c, g_rccl.group_start());
+            if (c->shard_rank == 0) {
+                for (int q = 1; q < c->shard_n; q++)
+                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(sl.gbuf) + (size_t)q * slice, slice, ncclUint8, q,
+                                            comm->comm, c->comm_stream));
+            } else {
+                NCCL_TRY(c, g_rccl.send(sl.tbuf, slice, ncclUint8, 0, comm->comm, c->comm_stream));
+            }
+            NCCL_TRY(c, g_rccl.group_end());
+            HIP_TRY(c, hipEventRecord(sl.gathered, c->comm_stream));
+            HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.gathered, 0));   // slot reuse after the send
+            if (c->shard_rank == 0)
+                st = rv_untile(c, sl.gbuf, c->shard_all.data(), (int32_t)c->shard_all.size(), T);
+            else
+                st = end_frame(c);
+        } else if (c->shard_n == 1) {   // one rank, no communicator: assemble locally
+            st = rv_untile(c, sl.tbuf, c->shard_all.data(), (int32_t)c->shard_all.size(), T);
+        }
+    }
+    c->ext_tilebuf = saved_ext; c->ext_tilebuf_bytes = saved_ext_bytes;
+    c->stream = caller;
+    if (st != RV_OK) return st;
+    // the caller's stream sees every frame of the loop complete
+    for (const FrameSlot& sl : c->slots)
+        if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(caller, sl.done, 0));
     return RV_OK;
 }
 

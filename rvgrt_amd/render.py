@@ -9,6 +9,7 @@ librvgrt_hip.so; errors raise RvError with rv_last_error().
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -36,6 +37,51 @@ def camera_dict(cam: rv_camera, vp):
     return {"pos": np.array(cam.pos[:], np.float32), "fo": np.array(cam.forward[:], np.float32),
             "ri": np.array(cam.right[:], np.float32), "up": np.array(cam.up[:], np.float32),
             "vp": np.asarray(vp, np.float32)}
+
+
+def rccl_path():
+    """The RCCL of the HIP runtime this process uses: torch's bundled librccl
+    when torch is already imported (the library then shares torch's runtime),
+    else None (the library loads the system librccl.so.1 next to the system
+    HIP runtime it was linked with)."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return None
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else None
+
+
+class Comm:
+    """RCCL communicator of one rank (rv_comm_*): rank 0 makes the unique id,
+    the caller broadcasts its 128 bytes, every rank creates its side."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id(path=None) -> bytes:
+        L = _lib.load()
+        buf = (C.c_ubyte * Comm.ID_BYTES)()
+        p = path if path is not None else rccl_path()
+        st = L.rv_comm_unique_id(p.encode() if p else None, C.cast(buf, C.c_void_p), Comm.ID_BYTES)
+        if st != 0:
+            raise RvError(f"rv_comm_unique_id: {_lib.STATUS_NAMES.get(st, st)}")
+        return bytes(buf)
+
+    def __init__(self, render: "StateRender", uid: bytes, nranks: int, rank: int, path=None):
+        self._L = _lib.load()
+        buf = (C.c_ubyte * Comm.ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        p = path if path is not None else rccl_path()
+        render._check(self._L.rv_comm_create(render._h, p.encode() if p else None, C.cast(buf, C.c_void_p),
+                                             Comm.ID_BYTES, int(nranks), int(rank), C.byref(h)), "rv_comm_create")
+        self._h = h
+        self.rank, self.nranks = int(rank), int(nranks)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rv_comm_destroy(self._h)
+            self._h = None
 
 
 class StateRender:
@@ -166,6 +212,22 @@ class StateRender:
         self._check(self._L.rv_frame_tiles(self._h, C.byref(cam), _ptr(vp), _ptr(pvp), float(time),
                                            float(jx), float(jy), f, _ptr(ids), len(ids),
                                            int(tile_px)), "rv_frame_tiles")
+
+    def set_tile_shard(self, tile_px, rank, nranks):
+        """This rank's interleaved share of T x T tiles for render_frames (0 ranks = full frames)."""
+        self._check(self._L.rv_set_tile_shard(self._h, int(tile_px), int(rank), int(nranks)), "rv_set_tile_shard")
+
+    def render_frames(self, n, cam, vp, prev_vp=None, time=0.0, jx=0.0, jy=0.0, flags=None,
+                      gi_per_frame=False, comm=None):
+        """Native frame loop (rv_render_frames): n frames over the frame slots'
+        streams; with a tile shard, this rank's tiles, the RCCL gather to rank 0
+        and rank 0's untile every frame."""
+        vp = np.ascontiguousarray(vp, np.float32)
+        pvp = vp if prev_vp is None else np.ascontiguousarray(prev_vp, np.float32)
+        f = self.flags if flags is None else int(flags)
+        self._check(self._L.rv_render_frames(self._h, int(n), C.byref(cam), _ptr(vp), _ptr(pvp), float(time),
+                                             float(jx), float(jy), f, int(bool(gi_per_frame)),
+                                             comm._h if comm is not None else None), "rv_render_frames")
 
     def tile_buffer(self):
         p, n = C.c_void_p(), C.c_size_t()

@@ -381,3 +381,40 @@ def test_frames_in_flight_identical(rv, atlas, flags):
     r.close()
     ref.close()
     hip.close()
+
+
+@pytest.mark.parametrize("flags", [8, 7])
+def test_render_frames_native_loop(rv, atlas, flags):
+    """rv_render_frames: the native loop over 3 frame slots equals frames
+    rendered one at a time -- whole frames, a one-rank tile shard assembled
+    locally, and the same shard gathered through a one-rank RCCL
+    communicator (the multi-GPU code path with no peers)."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H, T = 7, 320, 192, 64
+    gi = bool(flags & rv.RV_F_GI)
+    ref = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P1"], W, H)
+    r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    r.set_frames_in_flight(3)
+
+    def ref_frames(n):
+        for _ in range(n):
+            if gi:
+                ref.update_gi_data()
+            ref.frame(cam, vp)
+        return ref.readback(rv.RV_IMAGE_COLOR).copy()
+
+    r.render_frames(5, cam, vp, gi_per_frame=gi)
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref_frames(5))
+    r.set_tile_shard(T, 0, 1)
+    r.render_frames(4, cam, vp, gi_per_frame=gi)
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref_frames(4))
+    comm = rv.Comm(r, rv.Comm.unique_id(), 1, 0)
+    r.render_frames(7, cam, vp, gi_per_frame=gi, comm=comm)
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref_frames(7))
+    with pytest.raises(rv.RvError):   # shard / communicator mismatch
+        r.set_tile_shard(T, 0, 2)
+        r.render_frames(1, cam, vp, comm=comm)
+    comm.close()
+    r.close()
+    ref.close()
