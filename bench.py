@@ -92,9 +92,10 @@ def main():
                     help="N>1 collective backend; gloo (host-staged gather, ranks may share a GPU) "
                          "only rehearses the multi-rank path")
     ap.add_argument("--inflight", type=int, default=None,
-                    help="frames in flight (default 2 on one GPU, 4 with N>1): frame k renders on stream "
-                         "k %% n with its own frame slot (rv_set_frames_in_flight), so frame k+1 fills frame "
-                         "k's tail; 1 = one frame at a time")
+                    help="frame slots (default 8 on one GPU, 16 with N>1): the native loop renders groups of "
+                         "that many frames per launch (the group's tail is shared by its frames; its RCCL "
+                         "gather overlaps the next group); the Python loop puts frame k on stream k %% n; "
+                         "1 = one frame at a time")
     ap.add_argument("--loop", default="native", choices=["native", "python"],
                     help="frame loop: rv_render_frames (C++: slots, streams, RCCL gather, untile) or the "
                          "per-frame Python loop over the same library calls (torch.distributed gather)")
@@ -144,7 +145,9 @@ def main():
     torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     r.set_frame_path(args.path)
-    nfl = args.inflight if args.inflight is not None else (2 if world_size == 1 else 4)
+    # frame slots: per-frame GI updates serialise frames (each reads the grid
+    # the previous update wrote), so those configs render one frame at a time
+    nfl = args.inflight if args.inflight is not None else (1 if gi_per_frame else (8 if world_size == 1 else 16))
     nfl = max(1, nfl if args.path == "fused" else 1)
     r.set_frames_in_flight(nfl)
     # frame k is submitted on streams[k % nfl] (streams[0] = the context's stream)
@@ -283,13 +286,16 @@ def main():
 
     # Per-stage kernel times from HIP events on the context's streams, in a
     # separate pass so the events' own gaps stay out of the timed region.
-    n_stage_frames = min(args.steps, 10)
+    # The native loop renders groups of `fpl` frames per launch (frames per
+    # launch = frame slots, unless a per-frame GI update splits them): one
+    # timing record per launch, as rocprof sees them.
+    fpl = nfl if (native and not gi_per_frame and args.path == "fused") else 1
+    n_launches = max(1, min(args.steps // fpl, 10))
+    n_stage_frames = n_launches * fpl
     serial[0] = True
-    r.timing_enable(n_stage_frames)
-    if native:   # one frame at a time on the context's stream (rv_render_frames, 1 slot in use)
-        r.set_frames_in_flight(1)
+    r.timing_enable(n_launches)
+    if native:
         run_native(n_stage_frames)
-        r.set_frames_in_flight(nfl)
     else:
         for _ in range(n_stage_frames):
             step()
@@ -318,7 +324,7 @@ def main():
     fps = args.steps / elapsed
     mrays = rays_per_frame * fps / 1e6
 
-    nf = max(nframes, 1)
+    nf = max(nframes, 1)   # timed launches (of fpl frames each)
     render_ms = stage_ms[2] / nf
     pp_ms = stage_ms[1] / nf
     gi_ms = stage_ms[0] / nf
@@ -331,7 +337,7 @@ def main():
                     "shadow": "k_wf_shadow",
                     "water": "k_wf_water", "cones": "k_wf_cones", "shade": "k_wf_shade"}
     dom_ms = avg_stage_ms[dom]
-    dom_bytes = stage_bytes[dom]
+    dom_bytes = stage_bytes[dom] * fpl
     if world_size > 1:   # per-GPU: this rank's share of the stage's bytes
         dom_bytes = dom_bytes * len(my_tiles) / ntiles
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -340,19 +346,19 @@ def main():
     if os.path.exists(tpath) and world_size == 1:   # PMC summaries are of the one-GPU launch
         try:
             tj = json.load(open(tpath))
-            if tj.get("kernel", "").startswith(kernel_names[dom]):
+            if tj.get("kernel", "").startswith(kernel_names[dom]) and tj.get("frames_per_launch", 1) == fpl:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     g = st_stage[dom]        # counters of the dominant stage's launch (census frame)
-    gathers = g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]
+    gathers = (g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]) * fpl
     if world_size > 1:
         gathers = gathers * len(my_tiles) / ntiles
     gather_rate = gathers / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
     roofline = {"bound": "hbm", "kernel": kernel_names[dom], "achieved": round(achieved, 2),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
-                "avg_launch_ms": round(dom_ms, 4),
+                "avg_launch_ms": round(dom_ms, 4), "frames_per_launch": fpl,
                 # the limit that binds in practice: traversal gathers per second
                 # against the scattered-gather ceiling of the L1/texture path
                 "gathers_per_launch": int(gathers), "gather_rate": round(gather_rate / 1e9, 2),
@@ -388,6 +394,7 @@ def main():
             "cone_steps_per_frame": st_all["cone_steps"],
             "cone_steps_per_s": round(st_all["cone_steps"] * fps, 1),
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
+            "frames_per_launch": fpl,
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
             "loop": "native" if native else "python",

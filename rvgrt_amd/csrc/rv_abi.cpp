@@ -35,6 +35,7 @@ struct FrameSlot {
     int* chunk_order[2] = {nullptr, nullptr}; uint32_t* chunk_cost[2] = {nullptr, nullptr};
     int* tile_order = nullptr; uint32_t* tile_cost = nullptr; size_t tile_ord_cap = 0;
     int tiles_px = 0; uint32_t frames_since_order = 0;
+    uint64_t tiles_seen = ~0ull;
     hipEvent_t done = nullptr;    // recorded after the slot's last frame work
     bool pending = false;         // `done` has been recorded at least once
     hipStream_t last_stream = nullptr;   // stream of the slot's last frame
@@ -44,6 +45,17 @@ struct FrameSlot {
     uint32_t* tbuf = nullptr; size_t tbytes = 0;
     uint32_t* gbuf = nullptr; size_t gbytes = 0;
     hipEvent_t gathered = nullptr;      // recorded on the comm stream after the slot's gather
+};
+
+// rv_render_frames batches: B frames per launch, two sets in ping-pong (set
+// j & 1 also uses frame slot j & 1's scheduling state).
+struct BatchSet {
+    uint32_t* color = nullptr; uint32_t* mv = nullptr; uint16_t* depth = nullptr;
+    float* hdist = nullptr; float* hshadow = nullptr;
+    uint32_t* tbuf = nullptr; uint32_t* gbuf = nullptr;
+    int nb = 0; size_t slice = 0, gbytes = 0;   // allocated for
+    hipEvent_t rendered = nullptr, gathered = nullptr;
+    bool pending = false;
 };
 
 struct rv_ctx {
@@ -69,7 +81,9 @@ struct rv_ctx {
     unsigned long long* counters = nullptr;
     DevIds tiles;                 // rv_frame_tiles list (device copy, re-uploaded on change)
     DevIds untile_ids;            // rv_untile list
-    int tiles_px = 0;             // tile size of the cached list
+    int tiles_px = 0;             // tile size of the cached list (active slot)
+    uint64_t tiles_ver = 0;       // bumped when the device tile list changes
+    uint64_t tiles_seen = ~0ull;  // list version the active slot's order arrays are for
     std::vector<int> tile_ident;
     int* tile_order = nullptr; uint32_t* tile_cost = nullptr; size_t tile_ord_cap = 0;   // SCHED_COST per tile slot
     uint32_t* tilebuf = nullptr; size_t tilebuf_bytes = 0;
@@ -109,6 +123,8 @@ struct rv_ctx {
     int fstream_prio = 0;
     hipStream_t comm_stream = nullptr;   // rv_render_frames: RCCL gathers, in frame order
     hipEvent_t ev_loop = nullptr;        // scratch event of rv_render_frames
+    BatchSet bsets[2];
+    int batch_streams = 1;               // RV_BATCH_STREAMS: streams rv_render_frames' groups alternate over
     // rv_set_tile_shard: this rank's tiles and the gathered layout (rank 0)
     int shard_px = 0, shard_rank = 0, shard_n = 0, shard_max = 0;
     std::vector<int32_t> shard_ids, shard_all;
@@ -148,6 +164,7 @@ void slot_save(rv_ctx* c) {
     for (int g = 0; g < 2; g++) { sl.chunk_order[g] = c->chunk_order[g]; sl.chunk_cost[g] = c->chunk_cost[g]; }
     sl.tile_order = c->tile_order; sl.tile_cost = c->tile_cost; sl.tile_ord_cap = c->tile_ord_cap;
     sl.tiles_px = c->tiles_px; sl.frames_since_order = c->frames_since_order;
+    sl.tiles_seen = c->tiles_seen;
 }
 
 void slot_load(rv_ctx* c, int s) {
@@ -161,6 +178,7 @@ void slot_load(rv_ctx* c, int s) {
     for (int g = 0; g < 2; g++) { c->chunk_order[g] = sl.chunk_order[g]; c->chunk_cost[g] = sl.chunk_cost[g]; }
     c->tile_order = sl.tile_order; c->tile_cost = sl.tile_cost; c->tile_ord_cap = sl.tile_ord_cap;
     c->tiles_px = sl.tiles_px; c->frames_since_order = sl.frames_since_order;
+    c->tiles_seen = sl.tiles_seen;
 }
 
 // Images (rows padded to 256 B like a D3D12 placed footprint), half-res
@@ -299,6 +317,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (!slot_alloc(c, c->slots[0])) return cleanup_fail(RV_ERR_OOM, "frame slot");
     slot_load(c, 0);
     if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
+    if (const char* e = getenv("RV_BATCH_STREAMS")) c->batch_streams = atoi(e);
     if (const char* e = getenv("RV_GI_PRIO")) c->gi_low_prio = atoi(e);
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (hipMalloc(&c->counters, NSTAGE * NCNT * sizeof(unsigned long long)) != hipSuccess)
@@ -354,6 +373,12 @@ void rv_destroy(rv_ctx* c) {
     }
 #endif
     if (c->gi_stream) { hipStreamSynchronize(c->gi_stream); hipStreamDestroy(c->gi_stream); }
+    for (BatchSet& b : c->bsets) {
+        hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
+        hipFree(b.tbuf); hipFree(b.gbuf);
+        if (b.rendered) hipEventDestroy(b.rendered);
+        if (b.gathered) hipEventDestroy(b.gathered);
+    }
     for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
     if (c->comm_stream) hipStreamDestroy(c->comm_stream);
     if (c->ev_loop) hipEventDestroy(c->ev_loop);
@@ -386,6 +411,8 @@ static rv_status begin_frame(rv_ctx* c) {
         }
         sl.last_stream = c->stream;
         sl.submitted = c->frame_seq;
+    } else if (c->world_stream != c->stream) {
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_world, 0));
     }
     c->frame_seq++;
     return RV_OK;
@@ -447,7 +474,7 @@ rv_status rv_set_frame_path(rv_ctx* c, int32_t path) {
 }
 
 rv_status rv_set_frames_in_flight(rv_ctx* c, int32_t n) {
-    if (!c || n < 1 || n > 8) return RV_ERR_INVALID;
+    if (!c || n < 1 || n > 32) return RV_ERR_INVALID;
     if (n > 1 && !c->megakernel) return fail(c, RV_ERR_STATE, "frames in flight need the fused path");
     HIP_TRY(c, hipDeviceSynchronize());
     slot_save(c);
@@ -667,6 +694,7 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
     f.qcount = c->qcount;
     f.enq = c->enq;
     f.wtrace = c->wtrace;
+    f.nbatch = 1;
     return f;
 }
 
@@ -804,6 +832,37 @@ rv_status rv_draw_cuda(rv_ctx* c, const float pos[3], const float fo[3], const f
     return rv_frame(c, &cam, vp16, pvp16, time, jx, jy, c->cfg.flags);
 }
 
+// Device tile list (uploaded when it changes) and the active slot's
+// SCHED_COST order/cost arrays for it (identity order, zero costs whenever
+// the slot has not rendered this list yet).
+static rv_status tile_list(rv_ctx* c, const int32_t* tile_ids, int32_t ntiles, int32_t tile_px) {
+    bool changed = false;
+    rv_status us = upload_ids(c, c->tiles, tile_ids, ntiles, &changed);
+    if (us != RV_OK) return us;
+    if (changed) c->tiles_ver++;
+    if (c->tiles_seen != c->tiles_ver || tile_px != c->tiles_px) {
+        const size_t npad = ((size_t)ntiles + 7) & ~(size_t)7;
+        if (npad > c->tile_ord_cap) {
+            HIP_TRY(c, c->slots.size() > 1 ? hipDeviceSynchronize() : hipStreamSynchronize(c->stream));
+            hipFree(c->tile_order); hipFree(c->tile_cost);
+            c->tile_order = nullptr; c->tile_cost = nullptr; c->tile_ord_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->tile_order, npad * 4));
+            HIP_TRY(c, hipMalloc(&c->tile_cost, npad * 4));
+            c->tile_ord_cap = npad;
+        }
+        c->tile_ident.resize(npad);
+        for (size_t i = 0; i < npad; i++) c->tile_ident[i] = (int)i;
+        if (npad) {
+            HIP_TRY(c, hipMemcpyAsync(c->tile_order, c->tile_ident.data(), npad * 4, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemsetAsync(c->tile_cost, 0, npad * 4, c->stream));
+        }
+        c->tiles_px = tile_px;
+        c->tiles_seen = c->tiles_ver;
+        c->frames_since_order = 0;
+    }
+    return RV_OK;
+}
+
 rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, const float* pvp16, float time,
                          float jx, float jy, int32_t flags, const int32_t* tile_ids, int32_t ntiles,
                          int32_t tile_px) {
@@ -823,28 +882,7 @@ rv_status rv_frame_tiles(rv_ctx* c, const rv_camera* cam, const float* vp16, con
     }
     if (c->ext_tilebuf && need > c->ext_tilebuf_bytes) return fail(c, RV_ERR_INVALID, "bound tile buffer too small");
     if (rv_status bs = begin_frame(c)) return bs;
-    bool changed = false;
-    rv_status us = upload_ids(c, c->tiles, tile_ids, ntiles, &changed);
-    if (us != RV_OK) return us;
-    if (changed || tile_px != c->tiles_px) {   // new list: identity order, no costs yet
-        const size_t npad = ((size_t)ntiles + 7) & ~(size_t)7;
-        if (npad > c->tile_ord_cap) {
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-            hipFree(c->tile_order); hipFree(c->tile_cost);
-            c->tile_order = nullptr; c->tile_cost = nullptr; c->tile_ord_cap = 0;
-            HIP_TRY(c, hipMalloc(&c->tile_order, npad * 4));
-            HIP_TRY(c, hipMalloc(&c->tile_cost, npad * 4));
-            c->tile_ord_cap = npad;
-        }
-        c->tile_ident.resize(npad);
-        for (size_t i = 0; i < npad; i++) c->tile_ident[i] = (int)i;
-        if (npad) {
-            HIP_TRY(c, hipMemcpyAsync(c->tile_order, c->tile_ident.data(), npad * 4, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(c, hipMemsetAsync(c->tile_cost, 0, npad * 4, c->stream));
-        }
-        c->tiles_px = tile_px;
-        c->frames_since_order = 0;
-    }
+    if (rv_status ts = tile_list(c, tile_ids, ntiles, tile_px)) return ts;
     FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
     f.tiles = c->tiles.d; f.ntiles = ntiles; f.tile_px = tile_px; f.tiles_x = tiles_x;
     f.tilebuf = c->ext_tilebuf ? c->ext_tilebuf : c->tilebuf;
@@ -1156,6 +1194,148 @@ struct rv_comm {
             return fail((ctx), RV_ERR_HIP, std::string(#expr) + ": " + g_rccl.error_string(r_)); \
     } while (0)
 
+// Batched frame loop: groups of B = (frame slots) frames, each group one
+// launch per stage with the frame index in the grid (FrameParams::nbatch),
+// one RCCL gather of the group's packed tiles and one untile.  Group j runs
+// on stream j & 1 with batch set j & 1 and frame slot j & 1's scheduling
+// state, so group j+1 fills group j's tail while group j is gathered.
+static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
+                                const float* pvp16, float time, float jx, float jy, int32_t flags, rv_comm* comm,
+                                bool own0, hipStream_t caller, size_t slice) {
+    const int B = (int)c->slots.size();
+    const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
+    const int W = c->cfg.width, H = c->cfg.height, T = c->shard_px;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
+    const size_t gneed = tiles && root ? slice * (size_t)B * (size_t)c->shard_n : 0;
+    for (BatchSet& b : c->bsets) {
+        if (b.nb == B && b.slice == slice && b.gbytes == gneed) continue;
+        HIP_TRY(c, hipDeviceSynchronize());
+        hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
+        hipFree(b.tbuf); hipFree(b.gbuf);
+        b.color = nullptr; b.mv = nullptr; b.depth = nullptr; b.hdist = b.hshadow = nullptr;
+        b.tbuf = b.gbuf = nullptr; b.nb = 0; b.pending = false;
+        HIP_TRY(c, hipMalloc(&b.color, cstride * B));
+        HIP_TRY(c, hipMalloc(&b.mv, mstride * B));
+        HIP_TRY(c, hipMalloc(&b.depth, dstride * B));
+        HIP_TRY(c, hipMalloc(&b.hdist, hbytes * B));
+        HIP_TRY(c, hipMalloc(&b.hshadow, hbytes * B));
+        if (tiles) HIP_TRY(c, hipMalloc(&b.tbuf, slice * B));
+        if (gneed) HIP_TRY(c, hipMalloc(&b.gbuf, gneed));
+        if (!b.rendered) HIP_TRY(c, hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming));
+        if (!b.gathered) HIP_TRY(c, hipEventCreateWithFlags(&b.gathered, hipEventDisableTiming));
+        b.nb = B; b.slice = slice; b.gbytes = gneed;
+    }
+    // groups run on one stream by default (each launch then runs alone: its
+    // duration is the kernel's own, as rocprof reports it); RV_BATCH_STREAMS=2
+    // alternates two streams so a group's tail overlaps the next group
+    hipStream_t S[2] = {own0 ? c->fstreams[0] : caller, own0 ? c->fstreams[1] : c->fstreams[0]};
+    if (c->batch_streams < 2) S[1] = S[0];
+    slot_save(c);
+    if (tiles) {   // device tile lists and both slots' orders, on the caller's stream
+        c->stream = caller;
+        if (rv_status us = upload_ids(c, c->untile_ids, c->shard_all.data(), (int)c->shard_all.size(), nullptr)) return us;
+        for (int k = 0; k < 2; k++) {
+            slot_load(c, k);
+            if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
+            slot_save(c);
+        }
+    }
+    HIP_TRY(c, hipEventRecord(c->ev_loop, caller));
+    for (hipStream_t x : S) {   // the caller's work, the last world/GI write, frames of earlier calls
+        HIP_TRY(c, hipStreamWaitEvent(x, c->ev_loop, 0));
+        if (c->world_stream != x) HIP_TRY(c, hipStreamWaitEvent(x, c->ev_world, 0));
+        for (const FrameSlot& sl : c->slots)
+            if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(x, sl.done, 0));
+    }
+    int done = 0, last_nb = 0, last = 0;
+    for (int j = 0; done < frames; j++) {
+        const int nb = std::min(B, frames - done), k = j & 1;
+        BatchSet& bs = c->bsets[k];
+        c->stream = S[k];
+        slot_save(c);
+        slot_load(c, k);
+        if (bs.pending && tiles && !root) HIP_TRY(c, hipStreamWaitEvent(S[k], bs.gathered, 0));   // tile buffer reuse
+        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+        f.nbatch = (uint32_t)nb;
+        f.color = bs.color; f.color_pitch = c->own_color_pitch; f.bs_color = cstride;
+        f.mv = bs.mv; f.mv_pitch = c->own_mv_pitch; f.bs_mv = mstride;
+        f.depth = bs.depth; f.depth_pitch = c->own_depth_pitch; f.bs_depth = dstride;
+        f.hdist = bs.hdist; f.hshadow = bs.hshadow; f.bs_half = hbytes;
+        if (tiles) {
+            if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
+            f.tiles = c->tiles.d; f.ntiles = (int)c->shard_ids.size(); f.tile_px = T;
+            f.tiles_x = (W + T - 1) / T;
+            f.tilebuf = bs.tbuf; f.bs_tile = slice;
+            f.chunk_order[CG_RENDER] = c->tile_order; f.chunk_cost[CG_RENDER] = c->tile_cost;
+        }
+        if (rv_status rs = run_stages(c, f, tiles)) return rs;
+        c->frame_seq += (uint64_t)nb;
+        const int tx = (W + T - 1) / std::max(T, 1);
+        if (tiles && comm) {
+            HIP_TRY(c, hipEventRecord(bs.rendered, S[k]));
+            HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, bs.rendered, 0));
+            const size_t part = slice * (size_t)nb;   // one rank's frames of the group
+            if (root) HIP_TRY(c, hipMemcpyAsync(bs.gbuf, bs.tbuf, part, hipMemcpyDeviceToDevice, c->comm_stream));
+            NCCL_TRY(c, g_rccl.group_start());
+            if (root) {
+                for (int q = 1; q < c->shard_n; q++)
+                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(bs.gbuf) + (size_t)q * part, part, ncclUint8, q,
+                                            comm->comm, c->comm_stream));
+            } else {
+                NCCL_TRY(c, g_rccl.send(bs.tbuf, part, ncclUint8, 0, comm->comm, c->comm_stream));
+            }
+            NCCL_TRY(c, g_rccl.group_end());
+            HIP_TRY(c, hipEventRecord(bs.gathered, c->comm_stream));
+            if (root) {
+                HIP_TRY(c, hipStreamWaitEvent(S[k], bs.gathered, 0));
+                launch_untile(S[k], bs.gbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tx, W, H,
+                              bs.color, c->own_color_pitch, c->shard_max, nb, cstride);
+                LAUNCH_CHECK(c);
+            }
+        } else if (tiles && c->shard_n == 1) {   // one rank without a communicator: assemble locally
+            launch_untile(S[k], bs.tbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tx, W, H, bs.color,
+                          c->own_color_pitch, c->shard_max, nb, cstride);
+            LAUNCH_CHECK(c);
+        }
+        bs.pending = true;
+        done += nb; last_nb = nb; last = k;
+    }
+    // the last frame becomes slot 0's images (rv_readback / rv_image_ptr)
+    slot_save(c);
+    slot_load(c, 0);
+    c->stream = S[last];
+    const BatchSet& lb = c->bsets[last];
+    const size_t li = (size_t)(last_nb - 1);
+    if (!tiles || root) {
+        HIP_TRY(c, hipMemcpy2DAsync(c->color, c->color_pitch, reinterpret_cast<const char*>(lb.color) + li * cstride,
+                                    c->own_color_pitch, (size_t)W * 4, H, hipMemcpyDeviceToDevice, S[last]));
+        if (!tiles) {
+            HIP_TRY(c, hipMemcpy2DAsync(c->mv, c->mv_pitch, reinterpret_cast<const char*>(lb.mv) + li * mstride,
+                                        c->own_mv_pitch, (size_t)W * 4, H, hipMemcpyDeviceToDevice, S[last]));
+            HIP_TRY(c, hipMemcpy2DAsync(c->depth, c->depth_pitch, reinterpret_cast<const char*>(lb.depth) + li * dstride,
+                                        c->own_depth_pitch, (size_t)W * 2, H, hipMemcpyDeviceToDevice, S[last]));
+            HIP_TRY(c, hipMemcpyAsync(c->hdist, reinterpret_cast<const char*>(lb.hdist) + li * hbytes, hbytes,
+                                      hipMemcpyDeviceToDevice, S[last]));
+            HIP_TRY(c, hipMemcpyAsync(c->hshadow, reinterpret_cast<const char*>(lb.hshadow) + li * hbytes, hbytes,
+                                      hipMemcpyDeviceToDevice, S[last]));
+        }
+    }
+    // slot 0 is "done" when both groups' streams are: the caller's stream waits for all of it
+    HIP_TRY(c, hipEventRecord(c->ev_loop, S[last ^ 1]));
+    HIP_TRY(c, hipStreamWaitEvent(S[last], c->ev_loop, 0));
+    if (c->comm_stream) {
+        HIP_TRY(c, hipEventRecord(c->ev_loop, c->comm_stream));
+        HIP_TRY(c, hipStreamWaitEvent(S[last], c->ev_loop, 0));
+    }
+    FrameSlot& s0 = c->slots[0];
+    HIP_TRY(c, hipEventRecord(s0.done, S[last]));
+    s0.pending = true;
+    s0.last_stream = S[last];
+    HIP_TRY(c, hipStreamWaitEvent(caller, s0.done, 0));
+    return RV_OK;
+}
+
 extern "C" {
 
 rv_status rv_comm_unique_id(const char* rccl_path, void* id, size_t bytes) {
@@ -1232,11 +1412,21 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
     if (c->stream) HIP_TRY(c, hipStreamGetPriority(c->stream, &prio));
     if (!c->fstreams.empty() && c->fstream_prio != prio) {
         HIP_TRY(c, hipDeviceSynchronize());
-        for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
+        for (BatchSet& b : c->bsets) {
+        hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
+        hipFree(b.tbuf); hipFree(b.gbuf);
+        if (b.rendered) hipEventDestroy(b.rendered);
+        if (b.gathered) hipEventDestroy(b.gathered);
+    }
+    for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
         c->fstreams.clear();
     }
     c->fstream_prio = prio;
-    while ((int)c->fstreams.size() < n - 1) {
+    // slot 0 runs on the caller's stream unless that is the legacy NULL
+    // stream (which would serialise with the others): then on a stream of its own
+    const bool own0 = c->stream == nullptr;
+    const int nown = own0 ? n : n - 1;
+    while ((int)c->fstreams.size() < nown) {
         hipStream_t st;
         HIP_TRY(c, hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
         c->fstreams.push_back(st);
@@ -1264,9 +1454,15 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
     HIP_TRY(c, hipEventRecord(c->ev_loop, caller));
     for (hipStream_t fs : c->fstreams) HIP_TRY(c, hipStreamWaitEvent(fs, c->ev_loop, 0));
     if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_loop, 0));
+    if (!gi_per_frame && n > 1 && c->megakernel && frames > 0) {
+        st = render_batches(c, frames, cam, vp16, pvp16, time, jx, jy, flags, comm, own0, caller, slice);
+        c->ext_tilebuf = saved_ext; c->ext_tilebuf_bytes = saved_ext_bytes;
+        c->stream = caller;
+        return st;
+    }
     for (int k = 0; k < frames && st == RV_OK; k++) {
         const int s = (int)(c->frame_seq % (uint64_t)n);   // the slot begin_frame will pick
-        c->stream = s == 0 ? caller : c->fstreams[s - 1];
+        c->stream = own0 ? c->fstreams[s] : (s == 0 ? caller : c->fstreams[s - 1]);
         if (gi_per_frame && (st = rv_update_gi_data(c)) != RV_OK) break;
         if (!tiles) { st = rv_frame(c, cam, vp16, pvp16, time, jx, jy, flags); continue; }
         FrameSlot& sl = c->slots[s];
@@ -1304,6 +1500,10 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
     // the caller's stream sees every frame of the loop complete
     for (const FrameSlot& sl : c->slots)
         if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(caller, sl.done, 0));
+    if (c->slots.size() == 1 && own0) {   // one slot on an own stream: no slot event was recorded
+        HIP_TRY(c, hipEventRecord(c->ev_loop, c->fstreams[0]));
+        HIP_TRY(c, hipStreamWaitEvent(caller, c->ev_loop, 0));
+    }
     return RV_OK;
 }
 

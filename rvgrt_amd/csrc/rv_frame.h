@@ -28,6 +28,17 @@ __device__ __forceinline__ void block_count_flush(unsigned long long* counters, 
 
 static constexpr float SHADOW_HIT = 0.199951171875f;   // (float)(half)0.2f
 
+// Frame b of a batched launch: its outputs (wave-uniform, SGPR math).
+__device__ __forceinline__ void batch_frame(FrameParams& f, uint64_t b) {
+    if (b == 0) return;
+    f.color = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(f.color) + b * f.bs_color);
+    if (f.mv) f.mv = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(f.mv) + b * f.bs_mv);
+    if (f.depth) f.depth = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(f.depth) + b * f.bs_depth);
+    f.hdist = reinterpret_cast<float*>(reinterpret_cast<char*>(f.hdist) + b * f.bs_half);
+    f.hshadow = reinterpret_cast<float*>(reinterpret_cast<char*>(f.hshadow) + b * f.bs_half);
+    if (f.tilebuf) f.tilebuf = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(f.tilebuf) + b * f.bs_tile);
+}
+
 __device__ __forceinline__ f3 ray_dir(const FrameParams& f, float x, float y) {
     float nx = x * 2.0f - 1.0f + f.jx;   // StateRender.cu:44
     float ny = y * 2.0f - 1.0f + f.jy;

@@ -63,6 +63,10 @@ struct FrameParams {
     uint32_t qcap[NQUEUE];  // items per XCD sub-queue (sub-queue x at queue_wf[q] + x * qcap[q])
     int enq;                // queue append: 0 one atomic per wave, 1 per workgroup
     uint32_t* wtrace;       // RV_WAVE_TRACE builds: 8 dwords per k_render wave (diagnostics)
+    // frame batch (rv_render_frames): frame blockIdx.y of the launch writes
+    // images, half-res images and packed tiles this many bytes further on
+    uint64_t bs_color, bs_mv, bs_depth, bs_half, bs_tile;
+    uint32_t nbatch;        // frames in the launch (grid dimension of the frame index)
 };
 
 struct RvHitDev {   // == rv_hit
@@ -98,8 +102,10 @@ void launch_wf_shadow(hipStream_t s, const World& w, const FrameParams& f);
 void launch_wf_water(hipStream_t s, const World& w, const FrameParams& f);
 void launch_wf_cones(hipStream_t s, const World& w, const FrameParams& f);
 void launch_wf_shade(hipStream_t s, const World& w, const FrameParams& f, bool tiles);
+// Gathered buffer of a batch: rank q's B frames' slices back to back; slot i
+// of `ids` is entry i % per of rank i / per; frame b lands in color + b * bs.
 void launch_untile(hipStream_t s, const uint32_t* tiles, const int* ids, int ntiles, int tile_px, int tiles_x,
-                   int W, int H, uint32_t* color, size_t pitch);
+                   int W, int H, uint32_t* color, size_t pitch, int per = 0, int nbatch = 1, uint64_t bs = 0);
 void launch_trace_rays(hipStream_t s, const World& w, const float* org, const float* dir, const float* dist,
                        int64_t n, RvHitDev* out);
 

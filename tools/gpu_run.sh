@@ -22,16 +22,17 @@ for step in "$@"; do
                rc=$?; [ $rc -le 1 ] || exit 3 ;;
         bench) run bench 600 python bench.py || exit 3 ;;
         bench_c3) run bench_c3 600 python bench.py --config c3 --cpu-seconds 5 || exit 3 ;;
-        bench_c4) run bench_c4 600 python bench.py --config c4 --cpu-seconds 0 --steps 10 || exit 3 ;;
+        bench_c5) run bench_c5 600 python bench.py --config c5 --cpu-seconds 0 --steps 20 || exit 3 ;;
+        bench_c4) run bench_c4 600 python bench.py --config c4 --cpu-seconds 0 --steps 50 || exit 3 ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
-                  -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 || exit 3 ;;
+                  -o run -- python3 bench.py --cpu-seconds 0 || exit 3 ;;
         pmc) # PMC_SETS: counter sets separated by ';' (one rocprofv3 pass each)
              sets=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES;SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD"}
              IFS=';' read -ra SETS <<< "$sets"
              for ctr in "${SETS[@]}"; do
                  tag=$(echo $ctr | tr ' ' '_' | cut -c1-60)
                  run pmc_$tag 600 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/pmc_$tag \
-                     -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 ${BENCH_ARGS} || exit 3
+                     -o run -- python3 bench.py --steps 16 --warmup 8 --cpu-seconds 0 ${BENCH_ARGS} || exit 3
              done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -19,6 +19,7 @@ sys.path.insert(0, ROOT)
 
 
 def wall(fn, n):
+    fn()                     # warm: allocations and first-use set-up stay out of the timing
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n):
@@ -43,7 +44,8 @@ def main():
     quick = len(sys.argv) > 2 and sys.argv[2] == "quick"   # rv_frame + per-rank tile shares only
     W, H = cfg.width, cfg.height
     r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=load_atlas())
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     r.world_build()
     for s in range(max(cfg.gi_sweeps, 0)):
@@ -54,6 +56,15 @@ def main():
     n = 200
     out = {}
     out["frame"] = wall(lambda: r.frame(cam, vp), n)
+    # native loop, rank 0's share of an N-rank tile shard without the gather:
+    # the per-rank render rate the multi-GPU loop can reach
+    for N in (1, 8):
+        for K in [int(k) for k in os.environ.get("HO_K", "1,2,4,8").split(",")]:
+            r.set_frames_in_flight(K)
+            r.set_tile_shard(64, 0, N)
+            c, d = wall(lambda: r.render_frames(40, cam, vp), 10)
+            out[f"native_N{N}_K{K}"] = (c / 40, d / 40)
+    r.set_tile_shard(64, 0, 0)
     for K in (2, 3, 4):
         r.set_frames_in_flight(K)
         ss = [torch.cuda.Stream() for _ in range(K)]
@@ -65,6 +76,8 @@ def main():
             r.set_stream(ss[k].cuda_stream)
             r.frame(cam, vp)
         out[f"frame_K{K}"] = wall(frame_k, n)
+        c, d = wall(lambda: r.render_frames(20, cam, vp), n // 20)
+        out[f"native_full_K{K}"] = (c / 20, d / 20)
     r.set_frames_in_flight(1)
     r.set_stream(stream.cuda_stream)
     T = 64

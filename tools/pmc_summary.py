@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--kernel", default="k_render<false")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fpl", type=int, default=8, help="frames per launch of the profiled bench run")
     a = ap.parse_args()
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(a.dir, "pmc_*", "*counter_collection.csv")):
@@ -41,7 +42,7 @@ def main():
         raise SystemExit("no FETCH_SIZE rows for " + a.kernel)
     read_b = 2.0 * avg["FETCH_SIZE"] * 1024
     write_b = avg.get("WRITE_SIZE", 0.0) * 1024
-    out = {"kernel": a.kernel, "config": a.config,
+    out = {"kernel": a.kernel, "config": a.config, "frames_per_launch": a.fpl,
            "hbm_bytes_per_launch": int(read_b + write_b),
            "read_bytes_per_launch": int(read_b), "write_bytes_per_launch": int(write_b),
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 64-B tally of 128-B requests), write = WRITE_SIZE KiB",
