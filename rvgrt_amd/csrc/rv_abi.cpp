@@ -1249,6 +1249,15 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
             if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(x, sl.done, 0));
     }
     int done = 0, last_nb = 0, last = 0;
+    int prev_k = -1, prev_nb = 0;   // root: group gathered but not yet assembled
+    auto untile_group = [&](int kk, int nbb) -> rv_status {
+        BatchSet& g = c->bsets[kk];
+        HIP_TRY(c, hipStreamWaitEvent(S[kk], g.gathered, 0));
+        launch_untile(S[kk], g.gbuf, c->untile_ids.d, (int)c->shard_all.size(), T, (W + T - 1) / T, W, H, g.color,
+                      c->own_color_pitch, c->shard_max, nbb, cstride);
+        LAUNCH_CHECK(c);
+        return RV_OK;
+    };
     for (int j = 0; done < frames; j++) {
         const int nb = std::min(B, frames - done), k = j & 1;
         BatchSet& bs = c->bsets[k];
@@ -1287,11 +1296,10 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
             }
             NCCL_TRY(c, g_rccl.group_end());
             HIP_TRY(c, hipEventRecord(bs.gathered, c->comm_stream));
-            if (root) {
-                HIP_TRY(c, hipStreamWaitEvent(S[k], bs.gathered, 0));
-                launch_untile(S[k], bs.gbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tx, W, H,
-                              bs.color, c->own_color_pitch, c->shard_max, nb, cstride);
-                LAUNCH_CHECK(c);
+            if (root) {   // assemble the previous group now: its gather overlapped this group's render
+                if (prev_k >= 0)
+                    if (rv_status us = untile_group(prev_k, prev_nb)) return us;
+                prev_k = k; prev_nb = nb;
             }
         } else if (tiles && c->shard_n == 1) {   // one rank without a communicator: assemble locally
             launch_untile(S[k], bs.tbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tx, W, H, bs.color,
@@ -1301,6 +1309,8 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
         bs.pending = true;
         done += nb; last_nb = nb; last = k;
     }
+    if (prev_k >= 0)
+        if (rv_status us = untile_group(prev_k, prev_nb)) return us;
     // the last frame becomes slot 0's images (rv_readback / rv_image_ptr)
     slot_save(c);
     slot_load(c, 0);
