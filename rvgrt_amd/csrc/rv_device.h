@@ -300,7 +300,14 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 //     record are computed after it, so the per-step body is one 4-B gather
 //     plus ~20 VALU instructions.
 
-template <bool COUNT>
+// Build-time defaults of the traversal variants (kernels pick per launch
+// shape, see rv_kernels.hip): G = DDA look-ahead group, REUSE = keep the last
+// gathered word of each phase and gather again only when its address moves.
+#ifndef RV_WORD_REUSE
+#define RV_WORD_REUSE 0
+#endif
+
+template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0)>
 RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
     H.hit = false; H.undef = false; H.its = 0;
@@ -318,6 +325,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     int ix = 0, iy = 0, iz = 0, mask = -128;
     float tx = 0.0f, ty = 0.0f, tz = 0.0f;
     int status = 0;   // 0: gave up (miss), 2: left the grid (miss), 3: hit
+    uint32_t c_off = 0xFFFFFFFFu, c_word = 0, v_off = 0xFFFFFFFFu, v_word = 0;   // REUSE: last gathers
     for (int major = 0; major < 5; major++) {
         // ---- approximateCSDF: sphere-step through the coarse SDF.  The body
         // is straight-line (clamped, always-valid gather; predicated update)
@@ -329,7 +337,14 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
             const uint32_t cy = umin((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
             const uint32_t cz = umin((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
-            const uint32_t d = csdf_at(w, (int)cx, (int)cy, (int)cz);
+            uint32_t d;
+            if (REUSE) {   // gather only where the CSDF dword changed
+                const uint32_t off = csdf_off(w, cx, cy, cz);
+                if (off != c_off) { c_word = load_dword(w, off); c_off = off; }
+                d = csdf_byte(c_word, cx);
+            } else {
+                d = csdf_at(w, (int)cx, (int)cy, (int)cz);
+            }
             if (COUNT) sc.sphere += !oob;
             const bool stop = oob | (d <= 1);
             f3 nxt = add(cur, scale(dir, (float)d));
@@ -347,15 +362,14 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         mask = -128;
         int st = 0;           // 1: jump, 2: out of bounds, 3: hit
         uint32_t jd = 0;
-#if RV_DDA_GROUP > 1
+        if constexpr (G > 1) {
         // Look-ahead: the cells a DDA walk visits do not depend on the data
         // it reads (only where it stops does), so the next G cells' words --
         // and the CSDF word of an every-8th-step check among them -- are
         // gathered at once (G independent loads in flight instead of a chain
         // of G dependent ones), then the G steps are replayed in order on the
         // loaded words.  Loads past the step where the walk stops are unused.
-        constexpr int G = RV_DDA_GROUP;
-        static_assert(G == 2 || G == 4 || G == 8, "RV_DDA_GROUP divides 8");
+        static_assert(G == 2 || G == 4 || G == 8, "the look-ahead group divides 8");
         bool run = true;
         for (int i0 = 0; i0 < 200 && run; i0 += G) {
             uint32_t wv[G];
@@ -407,7 +421,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 if (!go) { run = false; break; }
             }
         }
-#else
+        } else {
         for (int i = 0; i < 200; i++) {
             if ((i & 7) == 7) {   // i is wave-uniform: a scalar branch
                 uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
@@ -420,7 +434,14 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
             // clamped (always valid) gather; its bit only counts in bounds
             const uint32_t qx = umin((uint32_t)ix, X - 1u), qy = umin((uint32_t)iy, Y - 1u), qz = umin((uint32_t)iz, Z - 1u);
-            const uint32_t word = load_dword(w, voxel_word_off(w, qx, qy, qz));
+            uint32_t word;
+            if (REUSE) {   // a word covers 8 (x) x 4 (y) voxels: runs along x/y re-read it
+                const uint32_t off = voxel_word_off(w, qx, qy, qz);
+                if (off != v_off) { v_word = load_dword(w, off); v_off = off; }
+                word = v_word;
+            } else {
+                word = load_dword(w, voxel_word_off(w, qx, qy, qz));
+            }
             const bool solid = (word >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
             if (COUNT) sc.dda += (st == 0) & !oob;
             st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
@@ -438,7 +459,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
             if (!go) break;
         }
-#endif
+        }
         if (st == 1) {        // empty space ahead: jump and restart
             f3 c = V((float)ix + 0.5f, (float)iy + 0.5f, (float)iz + 0.5f);
             float t = dot(sub(c, cur), dir);

@@ -1,7 +1,7 @@
 // rv_host_trace.cpp -- TEST INFRASTRUCTURE: the product's traversal source
 // (rvgrt_amd/csrc/rv_device.h, host+device functions) compiled for the CPU,
 // so tests/test_host_trace.py can check that exact code -- including its
-// compile-time variants (RV_DDA_GROUP look-ahead) -- against the oracle on
+// compile-time variants (DDA look-ahead group, word reuse) -- against the oracle on
 // hosts without a GPU.  Not linked into librvgrt_hip.so and not used by it.
 #include <stdint.h>
 #include <string.h>
@@ -48,6 +48,8 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
             }
     w.brick = h.brick.data();
 }
+template <int G, bool REUSE>
+Hit trace_v(const World& w, f3 o, f3 d, float t, StepCount& sc) { return trace<true, G, REUSE>(w, o, d, t, sc); }
 }  // namespace
 
 extern "C" {
@@ -55,16 +57,26 @@ extern "C" {
 // Out record per ray (48 B): pos[3], normal[3], u, v, hit, undef, sphere, dda, check (ints)
 struct HostHit { float pos[3], normal[3], u, v; int32_t hit, undef, sphere, dda, check, pad; };
 
-int rvh_dda_group(void) { return RV_DDA_GROUP; }
+// variant: 0..3 = DDA look-ahead group 1/2/4/8, 4 = group 1 with word reuse
+int rvh_variants(void) { return 5; }
 
-int rvh_trace_rays(int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
+int rvh_trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
                    const float* dir, const float* dist, int64_t n, HostHit* out) {
+    Hit (*fn)(const World&, f3, f3, float, StepCount&) = nullptr;
+    switch (variant) {
+    case 0: fn = trace_v<1, false>; break;
+    case 1: fn = trace_v<2, false>; break;
+    case 2: fn = trace_v<4, false>; break;
+    case 3: fn = trace_v<8, false>; break;
+    case 4: fn = trace_v<1, true>; break;
+    default: return -1;
+    }
     HostWorld h;
     build(h, lx, ly, lz, bits, csdf);
     for (int64_t i = 0; i < n; i++) {
         StepCount sc{};
-        Hit r = trace<true>(h.w, V(org[3 * i], org[3 * i + 1], org[3 * i + 2]),
-                            V(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), hround(dist[i]), sc);
+        Hit r = fn(h.w, V(org[3 * i], org[3 * i + 1], org[3 * i + 2]),
+                   V(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), hround(dist[i]), sc);
         HostHit& o = out[i];
         o.pos[0] = r.pos.x; o.pos[1] = r.pos.y; o.pos[2] = r.pos.z;
         o.normal[0] = r.normal.x; o.normal[1] = r.normal.y; o.normal[2] = r.normal.z;

@@ -1,7 +1,8 @@
 """The product's traversal source (rvgrt_amd/csrc/rv_device.h) compiled for
 the CPU (tests/host/rv_host_trace.cpp) against the oracle: hit, position,
 normal, uv and sphere/DDA/check step counts bit-exact on random rays, for
-every DDA look-ahead group size the GPU build can select (RV_DDA_GROUP).
+every traversal variant the GPU kernels can select (DDA look-ahead group
+1/2/4/8, word reuse).
 Runs without a GPU; the GPU build of the same source is checked by
 tests/test_gpu_parity.py::test_trace_bit_exact."""
 import ctypes as C
@@ -19,34 +20,34 @@ HIT = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("u", "<f4"), ("v", "<f
                 ("undef", "<i4"), ("sphere", "<i4"), ("dda", "<i4"), ("check", "<i4"), ("pad", "<i4")])
 
 
+VARIANTS = {"g1": 0, "g2": 1, "g4": 2, "g8": 3, "g1_reuse": 4}
+
+
 @pytest.fixture(scope="module")
-def host_libs():
+def host_lib():
     subprocess.run(["make", "-s", "-C", HOST], check=True)
-    libs = {}
-    for g in (1, 2, 4, 8):
-        L = C.CDLL(os.path.join(HOST, "build", f"librvhost_g{g}.so"))
-        L.rvh_trace_rays.restype = C.c_int
-        L.rvh_trace_rays.argtypes = [C.c_int] * 3 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p]
-        assert L.rvh_dda_group() == g
-        libs[g] = L
-    return libs
+    L = C.CDLL(os.path.join(HOST, "build", "librvhost.so"))
+    L.rvh_trace_rays.restype = C.c_int
+    L.rvh_trace_rays.argtypes = [C.c_int] * 4 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p]
+    assert L.rvh_variants() == len(VARIANTS)
+    return L
 
 
-def _trace(L, ow, org, d, dist):
+def _trace(L, variant, ow, org, d, dist):
     out = np.zeros(len(dist), HIT)
     p = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
-    assert L.rvh_trace_rays(ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(org), p(d), p(dist),
+    assert L.rvh_trace_rays(variant, ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(org), p(d), p(dist),
                             len(dist), p(out)) == 0
     return out
 
 
 @pytest.mark.parametrize("dims", [(7, 7, 7), (8, 6, 7)])
-@pytest.mark.parametrize("group", [1, 2, 4, 8])
-def test_host_trace_bit_exact(host_libs, oracle_world, dims, group):
+@pytest.mark.parametrize("variant", list(VARIANTS))
+def test_host_trace_bit_exact(host_lib, oracle_world, dims, variant):
     ow = oracle_world(*dims, gi_sweeps=0)
     rng = np.random.default_rng(4321)
     org, d, dist = random_rays(rng, 20000, (ow.X, ow.Y, ow.Z))
-    g = _trace(host_libs[group], ow, org, d, dist)
+    g = _trace(host_lib, VARIANTS[variant], ow, org, d, dist)
     o = ow.trace_batch(org, d, dist)
     assert (g["hit"] == o["hit"]).all()
     assert (g["undef"] == o["undef"]).all()
