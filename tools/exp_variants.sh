@@ -16,7 +16,7 @@ for v in ${VARIANTS:-main}; do
 import json; d=json.load(open('$out.json'))
 print('$v $cfg ms', d['ms_per_step'], {k: round(v, 4) for k, v in d['kernel_ms'].items() if v > 0.006}, 'frac', d['roofline']['frac'])"
   done
-  if [ -n "${TILES:-1}" ]; then
+  if [ "${TILES:-1}" = 1 ]; then
     RVGRT_LIB=$lib timeout -k 10 300 python tools/host_overhead.py ${TILECFG:-c2} quick > gpurun_out/var_${v}_tiles.log 2>&1 || exit 3
     grep "tiles_N\|^frame" gpurun_out/var_${v}_tiles.log | sed "s/^/$v /"
   fi
