@@ -203,13 +203,32 @@ def main():
     native = args.loop == "native" and (world_size == 1 or args.dist_backend == "nccl")
     comm = None
     if native and world_size > 1:
-        # RCCL communicator of the library (joins torch's librccl); id from rank 0
+        # RCCL communicator of the library (joins torch's librccl); id from rank 0.
+        # Any rank that cannot load RCCL or create its side makes every rank
+        # fall back to the Python loop's torch.distributed gather.
         r.set_tile_shard(T, rank, world_size)
-        uid = torch.zeros(rv.Comm.ID_BYTES, dtype=torch.uint8, device=dev)
+        uid = torch.zeros(rv.Comm.ID_BYTES + 1, dtype=torch.uint8, device=dev)
         if rank == 0:
-            uid.copy_(torch.tensor(list(rv.Comm.unique_id()), dtype=torch.uint8))
+            try:
+                uid[:-1].copy_(torch.tensor(list(rv.Comm.unique_id()), dtype=torch.uint8))
+                uid[-1] = 1
+            except rv.RvError as e:
+                log(f"[rank 0] rv_comm_unique_id failed ({e}); falling back to the Python loop")
         dist.broadcast(uid, src=0)
-        comm = rv.Comm(r, bytes(uid.cpu().tolist()), world_size, rank)
+        ok = torch.tensor([int(uid[-1].item())], dtype=torch.int32, device=dev)
+        if ok.item():
+            try:
+                comm = rv.Comm(r, bytes(uid[:-1].cpu().tolist()), world_size, rank)
+            except rv.RvError as e:
+                log(f"[rank {rank}] rv_comm_create failed ({e}); falling back to the Python loop")
+                ok.zero_()
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not ok.item():
+            if comm is not None:
+                comm.close()
+                comm = None
+            r.set_tile_shard(T, 0, 0)
+            native = False
 
     def run_native(k):
         r.set_stream(stream.cuda_stream)

@@ -1,4 +1,5 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "trace_bit_exact or frame_parity or gi_ or golden" > gpurun_out/par_main.log 2>&1; rc=$?; echo "parity main rc=$rc"; tail -1 gpurun_out/par_main.log; [ $rc -le 1 ] || exit 3
-TILES=x STEPS=200 CONFIGS="c2 c3 c4" VARIANTS="main slp" bash tools/exp_variants.sh 2>&1 | grep -v "tiles_\|frame"
+bash tools/gpu_run.sh smoke tests bench bench_c3 bench_c4 bench_c5 prof || exit 3
+timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 40 --warmup 5 --dist-backend gloo --cpu-seconds 0 > gpurun_out/mg_gloo2.log 2>&1; echo "gloo2 rc=$?"
+tail -1 gpurun_out/mg_gloo2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('gloo2', d['ms_per_step'], d['gather_check'], d['loop'], d['gather'])"
