@@ -28,6 +28,22 @@ __device__ __forceinline__ void block_count_flush(unsigned long long* counters, 
 
 static constexpr float SHADOW_HIT = 0.199951171875f;   // (float)(half)0.2f
 
+// Workgroup index and frame of a batched launch.  Interleaved (ileave = B > 1,
+// chunked grids whose x extent is a multiple of 8): XCD x's k-th workgroup
+// runs slot k / B of frame k % B, so the longest chunks of every frame of the
+// batch start first and no frame's tail trails the launch.  Otherwise the
+// frame is grid y.
+__device__ __forceinline__ uint32_t batch_block(const FrameParams& f, uint32_t& frame) {
+    uint32_t b = blockIdx.x;
+    frame = blockIdx.y;
+    if (f.ileave > 1) {
+        const uint32_t xcd = b & 7u, k = b >> 3;
+        frame = k % f.ileave;
+        b = ((k / f.ileave) << 3) | xcd;
+    }
+    return b;
+}
+
 // Frame b of a batched launch: its outputs (wave-uniform, SGPR math).
 __device__ __forceinline__ void batch_frame(FrameParams& f, uint64_t b) {
     if (b == 0) return;
@@ -75,10 +91,9 @@ __host__ __device__ inline uint32_t sched_grid(int sched, uint32_t w, uint32_t h
 // chunked grid and for regions off the image.
 template <uint32_t BW, uint32_t BH>
 __device__ __forceinline__ bool sched_block(int sched, const int* order, uint32_t w, uint32_t h, uint32_t& bx,
-                                            uint32_t& by) {
+                                            uint32_t& by, uint32_t b) {
     constexpr uint32_t CX = CHUNK_PX / BW, CY = CHUNK_PX / BH, PER = CX * CY;
     const uint32_t nbx = (w + BW - 1) / BW, nby = (h + BH - 1) / BH;
-    uint32_t b = blockIdx.x;
     if (sched == SCHED_CHUNK || sched == SCHED_COST) {
         // workgroup b runs on XCD b % 8: slot k of that XCD takes sorted chunk
         // (k / PER) * 8 + xcd, region k % PER inside it

@@ -66,7 +66,8 @@ struct FrameParams {
     // frame batch (rv_render_frames): frame blockIdx.y of the launch writes
     // images, half-res images and packed tiles this many bytes further on
     uint64_t bs_color, bs_mv, bs_depth, bs_half, bs_tile;
-    uint32_t nbatch;        // frames in the launch (grid dimension of the frame index)
+    uint32_t nbatch;        // frames in the launch
+    uint32_t ileave;        // > 1: frames interleaved along grid x (batch_block), else grid y = frame
 };
 
 struct RvHitDev {   // == rv_hit

@@ -123,7 +123,7 @@ __device__ __forceinline__ bool pixel_of(const FrameParams& f, int W, int H, int
         ix = tx * T + lx; iy = ty * T + ly;
         return lx < T && ly < T && ix < W && iy < H;
     }
-    if (!sched_block<16, 16>(f.sched, nullptr, W, H, bx, by)) { ix = iy = 0; return false; }
+    if (!sched_block<16, 16>(f.sched, nullptr, W, H, bx, by, blockIdx.x)) { ix = iy = 0; return false; }
     ix = (int)(bx * 16 + (wave & 1) * 8 + (lane & 7));
     iy = (int)(by * 16 + (wave >> 1) * 8 + (lane >> 3));
     return ix < W && iy < H;

@@ -1,5 +1,6 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-bash tools/gpu_run.sh smoke tests bench bench_c3 bench_c4 bench_c5 prof || exit 3
-timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 40 --warmup 5 --dist-backend gloo --cpu-seconds 0 > gpurun_out/mg_gloo2.log 2>&1; echo "gloo2 rc=$?"
-tail -1 gpurun_out/mg_gloo2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('gloo2', d['ms_per_step'], d['gather_check'], d['loop'], d['gather'])"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "in_flight or native_loop or tiles" > gpurun_out/tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -1 gpurun_out/tests.log; [ $rc -le 1 ] || exit 3
+TILES=x STEPS=400 CONFIGS="c2" VARIANTS="main noil main" bash tools/exp_variants.sh 2>&1
+HO_K=16 timeout -k 10 300 python tools/host_overhead.py c2 quick > gpurun_out/ho.log 2>&1 || exit 3
+grep "native_N8" gpurun_out/ho.log
