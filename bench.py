@@ -145,8 +145,11 @@ def main():
     torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     r.set_frame_path(args.path)
-    # frame slots: per-frame GI updates serialise frames (each reads the grid
-    # the previous update wrote), so those configs render one frame at a time
+    # frame slots = frames per group of the native loop.  A per-frame GI update
+    # serialises the renders (each reads the grid the previous update wrote):
+    # with slots only the pre-pass is grouped (--inflight 8: C3 0.435 -> 0.393
+    # ms, but C4 0.724 -> 0.816 ms: the GI kernel then overlaps only the
+    # render, not the pre-pass), so GI configs default to one frame at a time.
     nfl = args.inflight if args.inflight is not None else (1 if gi_per_frame else (8 if world_size == 1 else 16))
     nfl = max(1, nfl if args.path == "fused" else 1)
     r.set_frames_in_flight(nfl)
@@ -304,15 +307,19 @@ def main():
     elapsed = time.perf_counter() - t0
 
     # Per-stage kernel times from HIP events on the context's streams, in a
-    # separate pass so the events' own gaps stay out of the timed region.
-    # The native loop renders groups of `fpl` frames per launch (frames per
-    # launch = frame slots, unless a per-frame GI update splits them): one
-    # timing record per launch, as rocprof sees them.
-    fpl = nfl if (native and not gi_per_frame and args.path == "fused") else 1
-    n_launches = max(1, min(args.steps // fpl, 10))
-    n_stage_frames = n_launches * fpl
+    # separate pass of the same loop after the timed region, one record per
+    # launch, as rocprof sees them.  The native loop launches groups of nfl
+    # frames (frame slots); with a per-frame GI update only the pre-pass is
+    # grouped and the render runs frame by frame.
+    grouped = native and args.path == "fused" and nfl > 1
+    gi_groups = grouped and gi_per_frame and bool(flags & rv.RV_F_PREPASS) and world_size == 1
+    fpl = nfl if (grouped and not gi_per_frame) else 1
+    stage_fpl = {name: fpl for name in rv._lib.STAGES}
+    if gi_groups:
+        stage_fpl["pp_primary"] = nfl
+    n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if grouped else min(args.steps, 10)
     serial[0] = True
-    r.timing_enable(n_launches)
+    r.timing_enable(2 * n_stage_frames + 2)
     if native:
         run_native(n_stage_frames)
     else:
@@ -320,8 +327,8 @@ def main():
             step()
         drain()
     torch.cuda.synchronize(dev)
-    stage_ms, nframes = r.timing_get()
     per_stage_ms, _ = r.timing_stages()
+    launches = r.timing_launches()
     r.timing_enable(0)
     barrier()
     if dist is not None:
@@ -343,20 +350,22 @@ def main():
     fps = args.steps / elapsed
     mrays = rays_per_frame * fps / 1e6
 
-    nf = max(nframes, 1)   # timed launches (of fpl frames each)
-    render_ms = stage_ms[2] / nf
-    pp_ms = stage_ms[1] / nf
-    gi_ms = stage_ms[0] / nf
-    avg_stage_ms = {k: v / nf for k, v in per_stage_ms.items()}
-    # dominant kernel: the frame stage with the largest average launch time
-    dom = max((k for k in avg_stage_ms if k != "gi"), key=lambda k: avg_stage_ms[k])
+    # average launch time per stage, and its share of a frame
+    avg_stage_ms = {k: (per_stage_ms[k] / launches[k] if launches[k] else 0.0) for k in per_stage_ms}
+    frame_stage_ms = {k: avg_stage_ms[k] / stage_fpl[k] for k in avg_stage_ms}
+    gi_ms = frame_stage_ms["gi"]
+    pp_ms = frame_stage_ms["pp_primary"] + frame_stage_ms["pp_shadow"]
+    render_ms = sum(v for k, v in frame_stage_ms.items() if k not in ("gi", "pp_primary", "pp_shadow"))
+    # dominant kernel: the frame stage with the largest time per frame
+    dom = max((k for k in frame_stage_ms if k != "gi"), key=lambda k: frame_stage_ms[k])
     kernel_names = {"pp_primary": "k_prepass" if megakernel else "k_wf_pp_primary",
                     "pp_shadow": "k_wf_pp_shadow",
                     "primary": ("k_render_tiles" if world_size > 1 else "k_render") if megakernel else "k_wf_primary",
                     "shadow": "k_wf_shadow",
                     "water": "k_wf_water", "cones": "k_wf_cones", "shade": "k_wf_shade"}
     dom_ms = avg_stage_ms[dom]
-    dom_bytes = stage_bytes[dom] * fpl
+    dom_fpl = stage_fpl[dom]
+    dom_bytes = stage_bytes[dom] * dom_fpl
     if world_size > 1:   # per-GPU: this rank's share of the stage's bytes
         dom_bytes = dom_bytes * len(my_tiles) / ntiles
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -365,19 +374,19 @@ def main():
     if os.path.exists(tpath) and world_size == 1:   # PMC summaries are of the one-GPU launch
         try:
             tj = json.load(open(tpath))
-            if tj.get("kernel", "").startswith(kernel_names[dom]) and tj.get("frames_per_launch", 1) == fpl:
+            if tj.get("kernel", "").startswith(kernel_names[dom]) and tj.get("frames_per_launch", 1) == dom_fpl:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     g = st_stage[dom]        # counters of the dominant stage's launch (census frame)
-    gathers = (g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]) * fpl
+    gathers = (g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]) * dom_fpl
     if world_size > 1:
         gathers = gathers * len(my_tiles) / ntiles
     gather_rate = gathers / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
     roofline = {"bound": "hbm", "kernel": kernel_names[dom], "achieved": round(achieved, 2),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
-                "avg_launch_ms": round(dom_ms, 4), "frames_per_launch": fpl,
+                "avg_launch_ms": round(dom_ms, 4), "frames_per_launch": dom_fpl,
                 # the limit that binds in practice: traversal gathers per second
                 # against the scattered-gather ceiling of the L1/texture path
                 "gathers_per_launch": int(gathers), "gather_rate": round(gather_rate / 1e9, 2),
@@ -413,8 +422,8 @@ def main():
             "cone_steps_per_frame": st_all["cone_steps"],
             "cone_steps_per_s": round(st_all["cone_steps"] * fps, 1),
             "stage_ms": {"gi_update": round(gi_ms, 4), "prepass": round(pp_ms, 4), "render": round(render_ms, 4)},
-            "frames_per_launch": fpl,
-            "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},
+            "frames_per_launch": {k: v for k, v in stage_fpl.items() if launches.get(k)},
+            "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},   # per launch
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,

@@ -95,6 +95,7 @@ SIGNATURES = [
     ("rv_timing_enable", I32, [P, I32]),
     ("rv_timing_get", I32, [P, C.POINTER(C.c_double), C.POINTER(I32)]),
     ("rv_timing_stages", I32, [P, C.POINTER(C.c_double), I32, C.POINTER(I32)]),
+    ("rv_timing_launches", I32, [P, C.POINTER(I32), I32]),
     ("rv_sync", I32, [P]),
     ("rv_comm_unique_id", I32, [C.c_char_p, P, SZ]),
     ("rv_comm_create", I32, [P, C.c_char_p, P, SZ, I32, I32, C.POINTER(P)]),

@@ -720,7 +720,8 @@ static rv_status ensure_queues(rv_ctx* c, FrameParams& f, bool tiles) {
     return RV_OK;
 }
 
-static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
+// which: 1 = the pre-pass, 2 = the render (fused path), 3 = both.
+static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles, int which = 3) {
     if (!c->megakernel) {
         rv_status st = ensure_queues(c, f, tiles);
         if (st != RV_OK) return st;
@@ -739,16 +740,23 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles) {
     auto stage = [&](int k) { FrameParams g = f; g.counters = c->counters + (size_t)k * NCNT; return g; };
     const bool pre = (f.flags & RV_F_PREPASS) != 0;
     if (c->megakernel) {
-        if (pre) {
+        if (pre && (which & 1)) {
             HIP_TRY(c, mark(ST_PP_PRIMARY));
             if (tiles) launch_prepass_tiles(c->stream, w, stage(ST_PP_PRIMARY));
             else launch_prepass(c->stream, w, stage(ST_PP_PRIMARY));
             LAUNCH_CHECK(c);
         }
-        HIP_TRY(c, mark(ST_PRIMARY));
-        if (tiles) launch_render_tiles(c->stream, w, stage(ST_PRIMARY)); else launch_render(c->stream, w, stage(ST_PRIMARY));
-        LAUNCH_CHECK(c);
+        if (which & 2) {
+            HIP_TRY(c, mark(ST_PRIMARY));
+            if (tiles) launch_render_tiles(c->stream, w, stage(ST_PRIMARY)); else launch_render(c->stream, w, stage(ST_PRIMARY));
+            LAUNCH_CHECK(c);
+        }
         HIP_TRY(c, mark(-1));
+        if (!(which & 2)) {   // a pre-pass-only launch: orders are rebuilt after the renders
+            if (timed) c->ev_used[c->timing_n] = used;
+            if (timed) c->timing_n++;
+            return RV_OK;
+        }
         // SCHED_COST: re-order the chunks by the wave lifetimes (max over
         // the frames since the last ordering) every order_every frames; a
         // kernel boundary costs ~6 us, the ordering itself ~4 us.
@@ -940,6 +948,20 @@ rv_status rv_timing_stages(rv_ctx* c, double* ms, int32_t n, int32_t* frames) {
         }
     }
     if (frames) *frames = c->timing_n;
+    return RV_OK;
+}
+
+rv_status rv_timing_launches(rv_ctx* c, int32_t* counts, int32_t n) {
+    if (!c || !counts || n < 0) return RV_ERR_INVALID;
+    for (int k = 0; k < n; k++) counts[k] = 0;
+    for (int i = 0; i < c->timing_n; i++) {
+        const size_t e0 = (size_t)EV_PER_FRAME * i;
+        for (int j = 0; j + 1 < c->ev_used[i]; j++) {
+            const int k = c->ev_stage[e0 + j];
+            if (k >= 0 && k < n) counts[k]++;
+        }
+        if (c->gi_timed[i] && ST_GI < n) counts[ST_GI]++;
+    }
     return RV_OK;
 }
 
@@ -1194,6 +1216,97 @@ struct rv_comm {
             return fail((ctx), RV_ERR_HIP, std::string(#expr) + ": " + g_rccl.error_string(r_)); \
     } while (0)
 
+// Buffers of a batch set for B frames (images, half-res images, packed tiles
+// of `slice` bytes per frame, rank 0's gather buffer of `gneed` bytes).
+static rv_status bset_alloc(rv_ctx* c, BatchSet& b, int B, size_t slice, size_t gneed) {
+    if (b.nb == B && b.slice == slice && b.gbytes == gneed) return RV_OK;
+    const int H = c->cfg.height, W = c->cfg.width;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    HIP_TRY(c, hipDeviceSynchronize());
+    hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
+    hipFree(b.tbuf); hipFree(b.gbuf);
+    b.color = nullptr; b.mv = nullptr; b.depth = nullptr; b.hdist = b.hshadow = nullptr;
+    b.tbuf = b.gbuf = nullptr; b.nb = 0; b.pending = false;
+    HIP_TRY(c, hipMalloc(&b.color, c->own_color_pitch * H * B));
+    HIP_TRY(c, hipMalloc(&b.mv, c->own_mv_pitch * H * B));
+    HIP_TRY(c, hipMalloc(&b.depth, c->own_depth_pitch * H * B));
+    HIP_TRY(c, hipMalloc(&b.hdist, hbytes * B));
+    HIP_TRY(c, hipMalloc(&b.hshadow, hbytes * B));
+    if (slice) HIP_TRY(c, hipMalloc(&b.tbuf, slice * B));
+    if (gneed) HIP_TRY(c, hipMalloc(&b.gbuf, gneed));
+    if (!b.rendered) HIP_TRY(c, hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming));
+    if (!b.gathered) HIP_TRY(c, hipEventCreateWithFlags(&b.gathered, hipEventDisableTiming));
+    b.nb = B; b.slice = slice; b.gbytes = gneed;
+    return RV_OK;
+}
+
+// Copies frame `li` of a batch set into the active slot's images (the
+// context's current output, what rv_readback returns).
+static rv_status bset_publish(rv_ctx* c, const BatchSet& lb, size_t li, bool all, hipStream_t st) {
+    const int W = c->cfg.width, H = c->cfg.height;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
+    HIP_TRY(c, hipMemcpy2DAsync(c->color, c->color_pitch, reinterpret_cast<const char*>(lb.color) + li * cstride,
+                                c->own_color_pitch, (size_t)W * 4, H, hipMemcpyDeviceToDevice, st));
+    if (!all) return RV_OK;
+    HIP_TRY(c, hipMemcpy2DAsync(c->mv, c->mv_pitch, reinterpret_cast<const char*>(lb.mv) + li * mstride,
+                                c->own_mv_pitch, (size_t)W * 4, H, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpy2DAsync(c->depth, c->depth_pitch, reinterpret_cast<const char*>(lb.depth) + li * dstride,
+                                c->own_depth_pitch, (size_t)W * 2, H, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(c->hdist, reinterpret_cast<const char*>(lb.hdist) + li * hbytes, hbytes,
+                              hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(c->hshadow, reinterpret_cast<const char*>(lb.hshadow) + li * hbytes, hbytes,
+                              hipMemcpyDeviceToDevice, st));
+    return RV_OK;
+}
+
+// Frames with a per-frame GI update and the pre-pass (the reference frame,
+// C3-C5): the pre-pass reads only the static world, so it runs batched over
+// a group of B frames (one launch, frame index in the grid); then frame by
+// frame the GI update (kernel overlapping the previous render on the GI
+// stream) and the render, which reads its frame's half-res images.
+static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
+                                  const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S) {
+    const int B = (int)c->slots.size();
+    const int W = c->cfg.width, H = c->cfg.height;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
+    BatchSet& bs = c->bsets[0];
+    if (rv_status as = bset_alloc(c, bs, B, bs.slice, bs.gbytes)) return as;
+    slot_save(c);
+    slot_load(c, 0);
+    c->stream = S;
+    if (rv_status ws = wait_all_frames(c)) return ws;   // frames of earlier calls, the last world write
+    int done = 0, last = 0;
+    while (done < frames) {
+        const int nb = std::min(B, frames - done);
+        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+        f.nbatch = (uint32_t)nb;
+        f.hdist = bs.hdist; f.hshadow = bs.hshadow; f.bs_half = hbytes;
+        if (rv_status rs = run_stages(c, f, false, 1)) return rs;
+        for (int j = 0; j < nb; j++) {
+            if (rv_status gs = rv_update_gi_data(c)) return gs;
+            FrameParams g = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+            g.hdist = reinterpret_cast<float*>(reinterpret_cast<char*>(bs.hdist) + (size_t)j * hbytes);
+            g.hshadow = reinterpret_cast<float*>(reinterpret_cast<char*>(bs.hshadow) + (size_t)j * hbytes);
+            g.color = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(bs.color) + (size_t)j * cstride);
+            g.mv = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(bs.mv) + (size_t)j * mstride);
+            g.depth = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(bs.depth) + (size_t)j * dstride);
+            g.color_pitch = c->own_color_pitch; g.mv_pitch = c->own_mv_pitch; g.depth_pitch = c->own_depth_pitch;
+            if (rv_status rs = run_stages(c, g, false, 2)) return rs;
+            c->frame_seq++;
+            last = j;
+        }
+        done += nb;
+    }
+    if (rv_status ps = bset_publish(c, bs, (size_t)last, true, S)) return ps;
+    FrameSlot& s0 = c->slots[0];
+    HIP_TRY(c, hipEventRecord(s0.done, S));
+    s0.pending = true;
+    s0.last_stream = S;
+    return RV_OK;
+}
+
 // Batched frame loop: groups of B = (frame slots) frames, each group one
 // launch per stage with the frame index in the grid (FrameParams::nbatch),
 // one RCCL gather of the group's packed tiles and one untile.  Group j runs
@@ -1208,24 +1321,8 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
     const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
     const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
     const size_t gneed = tiles && root ? slice * (size_t)B * (size_t)c->shard_n : 0;
-    for (BatchSet& b : c->bsets) {
-        if (b.nb == B && b.slice == slice && b.gbytes == gneed) continue;
-        HIP_TRY(c, hipDeviceSynchronize());
-        hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
-        hipFree(b.tbuf); hipFree(b.gbuf);
-        b.color = nullptr; b.mv = nullptr; b.depth = nullptr; b.hdist = b.hshadow = nullptr;
-        b.tbuf = b.gbuf = nullptr; b.nb = 0; b.pending = false;
-        HIP_TRY(c, hipMalloc(&b.color, cstride * B));
-        HIP_TRY(c, hipMalloc(&b.mv, mstride * B));
-        HIP_TRY(c, hipMalloc(&b.depth, dstride * B));
-        HIP_TRY(c, hipMalloc(&b.hdist, hbytes * B));
-        HIP_TRY(c, hipMalloc(&b.hshadow, hbytes * B));
-        if (tiles) HIP_TRY(c, hipMalloc(&b.tbuf, slice * B));
-        if (gneed) HIP_TRY(c, hipMalloc(&b.gbuf, gneed));
-        if (!b.rendered) HIP_TRY(c, hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming));
-        if (!b.gathered) HIP_TRY(c, hipEventCreateWithFlags(&b.gathered, hipEventDisableTiming));
-        b.nb = B; b.slice = slice; b.gbytes = gneed;
-    }
+    for (BatchSet& b : c->bsets)
+        if (rv_status as = bset_alloc(c, b, B, slice, gneed)) return as;
     // groups run on one stream by default (each launch then runs alone: its
     // duration is the kernel's own, as rocprof reports it); RV_BATCH_STREAMS=2
     // alternates two streams so a group's tail overlaps the next group
@@ -1315,22 +1412,8 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
     slot_save(c);
     slot_load(c, 0);
     c->stream = S[last];
-    const BatchSet& lb = c->bsets[last];
-    const size_t li = (size_t)(last_nb - 1);
-    if (!tiles || root) {
-        HIP_TRY(c, hipMemcpy2DAsync(c->color, c->color_pitch, reinterpret_cast<const char*>(lb.color) + li * cstride,
-                                    c->own_color_pitch, (size_t)W * 4, H, hipMemcpyDeviceToDevice, S[last]));
-        if (!tiles) {
-            HIP_TRY(c, hipMemcpy2DAsync(c->mv, c->mv_pitch, reinterpret_cast<const char*>(lb.mv) + li * mstride,
-                                        c->own_mv_pitch, (size_t)W * 4, H, hipMemcpyDeviceToDevice, S[last]));
-            HIP_TRY(c, hipMemcpy2DAsync(c->depth, c->depth_pitch, reinterpret_cast<const char*>(lb.depth) + li * dstride,
-                                        c->own_depth_pitch, (size_t)W * 2, H, hipMemcpyDeviceToDevice, S[last]));
-            HIP_TRY(c, hipMemcpyAsync(c->hdist, reinterpret_cast<const char*>(lb.hdist) + li * hbytes, hbytes,
-                                      hipMemcpyDeviceToDevice, S[last]));
-            HIP_TRY(c, hipMemcpyAsync(c->hshadow, reinterpret_cast<const char*>(lb.hshadow) + li * hbytes, hbytes,
-                                      hipMemcpyDeviceToDevice, S[last]));
-        }
-    }
+    if (!tiles || root)
+        if (rv_status ps = bset_publish(c, c->bsets[last], (size_t)(last_nb - 1), !tiles, S[last])) return ps;
     // slot 0 is "done" when both groups' streams are: the caller's stream waits for all of it
     HIP_TRY(c, hipEventRecord(c->ev_loop, S[last ^ 1]));
     HIP_TRY(c, hipStreamWaitEvent(S[last], c->ev_loop, 0));
@@ -1470,9 +1553,19 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
         c->stream = caller;
         return st;
     }
+    if (gi_per_frame && (flags & RV_F_PREPASS) && !tiles && n > 1 && c->megakernel && frames > 0) {
+        hipStream_t S = own0 ? c->fstreams[0] : caller;
+        st = render_gi_groups(c, frames, cam, vp16, pvp16, time, jx, jy, flags, S);
+        c->stream = caller;
+        if (st != RV_OK) return st;
+        if (S != caller) HIP_TRY(c, hipStreamWaitEvent(caller, c->slots[0].done, 0));
+        return RV_OK;
+    }
     for (int k = 0; k < frames && st == RV_OK; k++) {
         const int s = (int)(c->frame_seq % (uint64_t)n);   // the slot begin_frame will pick
-        c->stream = own0 ? c->fstreams[s] : (s == 0 ? caller : c->fstreams[s - 1]);
+        // per-frame GI updates serialise the frames: one stream then
+        const int si = gi_per_frame ? 0 : s;
+        c->stream = own0 ? c->fstreams[si] : (si == 0 ? caller : c->fstreams[si - 1]);
         if (gi_per_frame && (st = rv_update_gi_data(c)) != RV_OK) break;
         if (!tiles) { st = rv_frame(c, cam, vp16, pvp16, time, jx, jy, flags); continue; }
         FrameSlot& sl = c->slots[s];

@@ -302,5 +302,12 @@ class StateRender:
         self._check(self._L.rv_timing_stages(self._h, ms, n, C.byref(k)), "rv_timing_stages")
         return dict(zip(_lib.STAGES, list(ms))), k.value
 
+    def timing_launches(self):
+        """{stage name: launches timed} (divide timing_stages' sums by these)."""
+        n = len(_lib.STAGES)
+        k = (C.c_int32 * n)()
+        self._check(self._L.rv_timing_launches(self._h, k, n), "rv_timing_launches")
+        return dict(zip(_lib.STAGES, list(k)))
+
     def stats_reset(self):
         self._check(self._L.rv_stats_reset(self._h), "rv_stats_reset")
