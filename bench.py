@@ -77,7 +77,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", help="c1..c5 (default c2 = BASELINE configs[1])")
     ap.add_argument("--pose", default="P0")
-    ap.add_argument("--tile-px", type=int, default=64)
+    ap.add_argument("--tile-px", type=int, default=None,
+                    help="screen-tile size of the N>1 shard (default: 16 px without the pre-pass, 32 with it; "
+                         "tools/shard_probe.py: C2 at 8 ranks renders its slowest share in 19.6 us/frame at "
+                         "16 px vs 30.9 at 64 px)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
@@ -88,6 +91,9 @@ def main():
     ap.add_argument("--gi-per-frame", type=int, default=None,
                     help="experiments only: override the config's per-frame GI update (0/1)")
     ap.add_argument("--gi-async", type=int, default=1, help="overlap the GI update with the previous render")
+    ap.add_argument("--pipe", type=int, default=1,
+                    help="native loop, per-frame GI + pre-pass (C3-C5), one GPU: one k_ref_pipe launch per frame "
+                         "runs render k | GI update k+1 | pre-pass k+1 (0: one frame at a time)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collective backend; gloo (host-staged gather, ranks may share a GPU) "
                          "only rehearses the multi-rank path")
@@ -156,6 +162,7 @@ def main():
     # frame k is submitted on streams[k % nfl] (streams[0] = the context's stream)
     streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.stream_priority) for _ in range(nfl - 1)]
     r.set_gi_async(args.gi_async)
+    r.set_pipeline(args.pipe)
     t0 = time.perf_counter()
     r.world_build()
     for s in range(max(cfg.gi_sweeps, 0)):
@@ -174,6 +181,14 @@ def main():
     st_all = r.stats(-1)
     st_stage = {name: r.stats(k) for k, name in enumerate(rv._lib.STAGES)}
     rays_per_frame = st_all["traces"]
+    gi_stats = None
+    if gi_per_frame:   # one UpdateGIData with step counters on: the GI update's algorithmic bytes
+        r.set_gi_stats(1)
+        r.stats_reset()
+        r.update_gi_data()
+        r.sync()
+        gi_stats = r.stats(rv._lib.STAGES.index("gi"))
+        r.set_gi_stats(0)
     megakernel = args.path == "fused"
     pp_hits = st_stage["pp_shadow"]["prepass_shadow"]
     stage_bytes = {name: algorithmic_bytes(st_stage[name], W * H, (W // 2) * (H // 2), prepass,
@@ -181,9 +196,13 @@ def main():
                                            if megakernel else name,
                                            pp_hits)
                    for name in rv._lib.STAGES if name != "gi"}
+    if gi_stats is not None:   # traversal + 16 B texel + 4 B bounce GI read per texture sample, 8 B per cell
+        gi_cells = min(262144, (cfg.n // 4) ** 3)
+        stage_bytes["gi"] = (4 * gi_stats["dda_steps"] + gi_stats["sphere_steps"] + gi_stats["csdf_checks"]
+                             + 20 * gi_stats["tex_samples"] + 8 * gi_cells)
 
     # ---------------------------------------------------------------- tiles
-    T = args.tile_px
+    T = args.tile_px if args.tile_px else (32 if prepass else 16)
     tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
     ntiles = tiles_x * tiles_y
     my_tiles = np.arange(rank, ntiles, world_size, dtype=np.int32)
@@ -312,7 +331,10 @@ def main():
     # frames (frame slots); with a per-frame GI update only the pre-pass is
     # grouped and the render runs frame by frame.
     grouped = native and args.path == "fused" and nfl > 1
-    gi_groups = grouped and gi_per_frame and bool(flags & rv.RV_F_PREPASS) and world_size == 1
+    # pipelined reference frames: every launch is k_ref_pipe (timed as stage "primary")
+    piped = (native and args.path == "fused" and args.pipe and gi_per_frame and bool(flags & rv.RV_F_PREPASS)
+             and world_size == 1)
+    gi_groups = grouped and gi_per_frame and bool(flags & rv.RV_F_PREPASS) and world_size == 1 and not piped
     fpl = nfl if (grouped and not gi_per_frame) else 1
     stage_fpl = {name: fpl for name in rv._lib.STAGES}
     if gi_groups:
@@ -360,12 +382,15 @@ def main():
     dom = max((k for k in frame_stage_ms if k != "gi"), key=lambda k: frame_stage_ms[k])
     kernel_names = {"pp_primary": "k_prepass" if megakernel else "k_wf_pp_primary",
                     "pp_shadow": "k_wf_pp_shadow",
-                    "primary": ("k_render_tiles" if world_size > 1 else "k_render") if megakernel else "k_wf_primary",
+                    "primary": ("k_ref_pipe" if piped else "k_render_tiles" if world_size > 1 else "k_render")
+                    if megakernel else "k_wf_primary",
                     "shadow": "k_wf_shadow",
                     "water": "k_wf_water", "cones": "k_wf_cones", "shade": "k_wf_shade"}
     dom_ms = avg_stage_ms[dom]
     dom_fpl = stage_fpl[dom]
     dom_bytes = stage_bytes[dom] * dom_fpl
+    if piped and dom == "primary":   # the launch also runs the next frame's pre-pass and GI update
+        dom_bytes = stage_bytes["primary"] + stage_bytes["pp_primary"] + stage_bytes.get("gi", 0)
     if world_size > 1:   # per-GPU: this rank's share of the stage's bytes
         dom_bytes = dom_bytes * len(my_tiles) / ntiles
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -380,6 +405,9 @@ def main():
             traffic = None
     g = st_stage[dom]        # counters of the dominant stage's launch (census frame)
     gathers = (g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]) * dom_fpl
+    if piped and dom == "primary":
+        for h in (st_stage["pp_primary"], gi_stats):
+            gathers += h["sphere_steps"] + h["dda_steps"] + h["csdf_checks"]
     if world_size > 1:
         gathers = gathers * len(my_tiles) / ntiles
     gather_rate = gathers / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
@@ -425,6 +453,7 @@ def main():
             "frames_per_launch": {k: v for k, v in stage_fpl.items() if launches.get(k)},
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},   # per launch
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
+            "pipelined": bool(piped),
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,
             "gather_check": gather_check,

@@ -70,6 +70,8 @@ SIGNATURES = [
     ("rv_set_stream", I32, [P, P]),
     ("rv_set_frame_path", I32, [P, I32]),
     ("rv_set_gi_async", I32, [P, I32]),
+    ("rv_set_pipeline", I32, [P, I32]),
+    ("rv_set_gi_stats", I32, [P, I32]),
     ("rv_set_frames_in_flight", I32, [P, I32]),
     ("rv_world_build", I32, [P]),
     ("rv_world_import", I32, [P, I32, P, SZ]),

@@ -115,6 +115,11 @@ struct rv_ctx {
     bool world_ready = false;
     int sched = SCHED_COST;
     int order_every = 4;          // RV_ORDER_EVERY: frames between chunk re-orderings
+    int pipe = 1;                 // rv_set_pipeline / RV_PIPE: pipelined reference frames
+    uint32_t pipe_order = 0x012;  // RV_PIPE_ORDER: dispatch order of the parts, hex digits PIPE_* (first = high)
+    float* pipe_half[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [k & 1] {dist, shadow}
+    bool gi_stats = false;        // rv_set_gi_stats
+    int gather_bpp = 3;           // RV_GATHER_BPP: packed pixel bytes of rv_render_frames' tile gather (3 or 4)
     uint32_t frames_since_order = 0;
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
     uint32_t* chunk_cost[2] = {nullptr, nullptr};
@@ -320,6 +325,13 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_BATCH_STREAMS")) c->batch_streams = atoi(e);
     if (const char* e = getenv("RV_GI_PRIO")) c->gi_low_prio = atoi(e);
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
+    if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
+    if (const char* e = getenv("RV_GATHER_BPP")) c->gather_bpp = atoi(e) == 4 ? 4 : 3;
+    if (const char* e = getenv("RV_PIPE_ORDER")) {   // a permutation of the parts, else the default
+        const uint32_t o = (uint32_t)strtoul(e, nullptr, 16);
+        const uint32_t a = o >> 8 & 0xF, b = o >> 4 & 0xF, d = o & 0xF;
+        if (o <= 0x210 && a < 3 && b < 3 && d < 3 && a != b && b != d && a != d) c->pipe_order = o;
+    }
     if (hipMalloc(&c->counters, NSTAGE * NCNT * sizeof(unsigned long long)) != hipSuccess)
         return cleanup_fail(RV_ERR_OOM, "counters");
     hipMemset(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long));
@@ -355,6 +367,7 @@ void rv_destroy(rv_ctx* c) {
     hipSetDevice(c->device);
     hipDeviceSynchronize();   // every frame slot's stream
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
+    for (auto& ph : c->pipe_half) { hipFree(ph[0]); hipFree(ph[1]); }
     if (!c->slots.empty()) slot_save(c);
     for (FrameSlot& sl : c->slots) slot_free(sl);
     hipFree(c->counters);
@@ -499,6 +512,18 @@ rv_status rv_set_gi_async(rv_ctx* c, int32_t on) {
     return RV_OK;
 }
 
+rv_status rv_set_pipeline(rv_ctx* c, int32_t on) {
+    if (!c) return RV_ERR_INVALID;
+    c->pipe = on != 0;
+    return RV_OK;
+}
+
+rv_status rv_set_gi_stats(rv_ctx* c, int32_t on) {
+    if (!c) return RV_ERR_INVALID;
+    c->gi_stats = on != 0;
+    return RV_OK;
+}
+
 rv_status rv_sync(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -629,7 +654,7 @@ static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t c
             if (sl.pending && sl.submitted < c->gi_swapped_at) HIP_TRY(c, hipStreamWaitEvent(ks, sl.done, 0));
     if (t0) HIP_TRY(c, hipEventRecord(t0, ks));
     launch_gi_update(ks, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count,
-                     c->counters + ST_GI * NCNT);
+                     c->counters + ST_GI * NCNT, c->gi_stats);
     LAUNCH_CHECK(c);
     if (t1) HIP_TRY(c, hipEventRecord(t1, ks));
     if (async) {
@@ -1307,6 +1332,103 @@ static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* ca
     return RV_OK;
 }
 
+// Pipelined reference frames (rv_set_pipeline; rvgrt.h).  On stream S:
+//   prologue  GI update of frame 0 (kernel + copy-back), pre-pass of frame 0;
+//   launch k  render k | GI update k+1 (grid k -> scratch) | pre-pass k+1,
+//             one k_ref_pipe grid (the last launch renders only);
+//   then      copy-back of update k+1's cells: in stream order after render
+//             k, the last reader of grid k, and before render k+1.
+// The half-res images alternate between two pairs (frame k & 1).
+static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
+                                const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S) {
+    const int W = c->cfg.width, H = c->cfg.height;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    for (auto& ph : c->pipe_half)
+        for (int q = 0; q < 2; q++)
+            if (!ph[q]) HIP_TRY(c, hipMalloc(&ph[q], hbytes));
+    if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
+    slot_save(c);
+    slot_load(c, 0);
+    c->stream = S;
+    if (rv_status ws = wait_all_frames(c)) return ws;   // frames of earlier calls, the last world write
+    const uint64_t n = n_gi(c), rays = c->cfg.gi_rays_per_frame;
+    auto next_range = [&](uint32_t& fr, uint64_t& first, uint64_t& count) {   // rv_update_gi_data's walk
+        fr = c->gi_frame;
+        first = c->gi_offset;
+        count = first + rays > n ? n - first : rays;
+        c->gi_frame++;
+        if (c->gi_offset + rays >= n) c->gi_offset = 0;   // src/CoarseArray.cu:392-394
+        else c->gi_offset += rays;
+    };
+    const World w = current_world(c);
+    unsigned long long* cnt_gi = c->counters + (size_t)ST_GI * NCNT;
+    uint32_t fr = 0;
+    uint64_t first = 0, count = 0;
+    next_range(fr, first, count);
+    launch_gi_update(S, c->gi, c->gi_tmp, w, sun_dir(), fr, first, count, cnt_gi, c->gi_stats);
+    LAUNCH_CHECK(c);
+    HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+    {
+        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+        f.hdist = c->pipe_half[0][0]; f.hshadow = c->pipe_half[0][1];
+        f.counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
+        launch_prepass(S, w, f);
+        LAUNCH_CHECK(c);
+    }
+    for (int k = 0; k < frames; k++) {
+        const bool more = k + 1 < frames;
+        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+        f.hdist = c->pipe_half[k & 1][0]; f.hshadow = c->pipe_half[k & 1][1];
+        f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
+        PipeParams p{};
+        p.gi_prev = c->gi; p.gi_next = c->gi_tmp;
+        if (more) next_range(p.gi_frame, first, count);
+        p.gi_first = first; p.gi_count = more ? count : 0;
+        p.pp_hdist = c->pipe_half[(k + 1) & 1][0]; p.pp_hshadow = c->pipe_half[(k + 1) & 1][1];
+        p.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
+        p.gi_counters = cnt_gi;
+        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, count) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
+                                  pipe_len(f, PIPE_RENDER, 0)};
+        for (int i = 0; i < 3; i++) {
+            p.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;
+            p.len[i] = lens[p.part[i]];
+        }
+        // timing (rv_timing_stages: stage ST_PRIMARY) records the full launches
+        const bool timed = (more || frames == 1) && c->timing_n < c->timing_cap;
+        const size_t e0 = (size_t)EV_PER_FRAME * c->timing_n;
+        if (timed) { c->ev_stage[e0] = ST_PRIMARY; HIP_TRY(c, hipEventRecord(c->ev[e0], S)); }
+        launch_ref_pipe(S, w, f, p);
+        LAUNCH_CHECK(c);
+        if (timed) {
+            c->ev_stage[e0 + 1] = -1;
+            HIP_TRY(c, hipEventRecord(c->ev[e0 + 1], S));
+            c->ev_used[c->timing_n] = 2;
+            c->timing_n++;
+        }
+        if (more)
+            HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+        if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
+            c->frames_since_order = 0;
+            launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
+                               n_chunks_pad(f.hw, f.hh));
+            launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
+                               n_chunks_pad(f.W, f.H));
+            LAUNCH_CHECK(c);
+        }
+        c->frame_seq++;
+    }
+    // the last frame's half-res images become the slot's (rv_readback)
+    const int lk = (frames - 1) & 1;
+    HIP_TRY(c, hipMemcpyAsync(c->hdist, c->pipe_half[lk][0], hbytes, hipMemcpyDeviceToDevice, S));
+    HIP_TRY(c, hipMemcpyAsync(c->hshadow, c->pipe_half[lk][1], hbytes, hipMemcpyDeviceToDevice, S));
+    if (rv_status ms = mark_world(c)) return ms;
+    FrameSlot& s0 = c->slots[0];
+    HIP_TRY(c, hipEventRecord(s0.done, S));
+    s0.pending = true;
+    s0.last_stream = S;
+    return RV_OK;
+}
+
 // Batched frame loop: groups of B = (frame slots) frames, each group one
 // launch per stage with the frame index in the grid (FrameParams::nbatch),
 // one RCCL gather of the group's packed tiles and one untile.  Group j runs
@@ -1318,6 +1440,9 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
     const int B = (int)c->slots.size();
     const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
     const int W = c->cfg.width, H = c->cfg.height, T = c->shard_px;
+    // packed tiles travel as RGB24 (alpha is always 255): 3/4 of the gather bytes
+    const int bpp = c->gather_bpp;
+    if (tiles) slice = (size_t)c->shard_max * T * T * bpp;
     const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
     const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
     const size_t gneed = tiles && root ? slice * (size_t)B * (size_t)c->shard_n : 0;
@@ -1351,7 +1476,7 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
         BatchSet& g = c->bsets[kk];
         HIP_TRY(c, hipStreamWaitEvent(S[kk], g.gathered, 0));
         launch_untile(S[kk], g.gbuf, c->untile_ids.d, (int)c->shard_all.size(), T, (W + T - 1) / T, W, H, g.color,
-                      c->own_color_pitch, c->shard_max, nbb, cstride);
+                      c->own_color_pitch, c->shard_max, nbb, cstride, bpp);
         LAUNCH_CHECK(c);
         return RV_OK;
     };
@@ -1372,7 +1497,7 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
             if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
             f.tiles = c->tiles.d; f.ntiles = (int)c->shard_ids.size(); f.tile_px = T;
             f.tiles_x = (W + T - 1) / T;
-            f.tilebuf = bs.tbuf; f.bs_tile = slice;
+            f.tilebuf = bs.tbuf; f.bs_tile = slice; f.tile_bpp = bpp;
             f.chunk_order[CG_RENDER] = c->tile_order; f.chunk_cost[CG_RENDER] = c->tile_cost;
         }
         if (rv_status rs = run_stages(c, f, tiles)) return rs;
@@ -1400,7 +1525,7 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
             }
         } else if (tiles && c->shard_n == 1) {   // one rank without a communicator: assemble locally
             launch_untile(S[k], bs.tbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tx, W, H, bs.color,
-                          c->own_color_pitch, c->shard_max, nb, cstride);
+                          c->own_color_pitch, c->shard_max, nb, cstride, bpp);
             LAUNCH_CHECK(c);
         }
         bs.pending = true;
@@ -1552,6 +1677,14 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
         c->ext_tilebuf = saved_ext; c->ext_tilebuf_bytes = saved_ext_bytes;
         c->stream = caller;
         return st;
+    }
+    if (gi_per_frame && (flags & RV_F_PREPASS) && !tiles && c->pipe && c->megakernel && frames > 0) {
+        hipStream_t S = own0 ? c->fstreams[0] : caller;
+        st = render_gi_pipe(c, frames, cam, vp16, pvp16, time, jx, jy, flags, S);
+        c->stream = caller;
+        if (st != RV_OK) return st;
+        if (S != caller) HIP_TRY(c, hipStreamWaitEvent(caller, c->slots[0].done, 0));
+        return RV_OK;
     }
     if (gi_per_frame && (flags & RV_F_PREPASS) && !tiles && n > 1 && c->megakernel && frames > 0) {
         hipStream_t S = own0 ? c->fstreams[0] : caller;

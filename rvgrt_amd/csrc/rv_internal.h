@@ -53,6 +53,7 @@ struct FrameParams {
     unsigned long long* counters;
     const int* tiles; int ntiles; int tile_px; int tiles_x;
     uint32_t* tilebuf;
+    int tile_bpp;           // packed tile pixels: 4 = RGBA8 (rv_frame_tiles), 3 = RGB24 (native loop's gather)
     // wavefront buffers (full res unless noted)
     float4* hpos;           // primary hit position xyz, w = uv half bits (u | v << 16)
     uint32_t* hinfo;        // HI_* flags | normal code << HI_NSHIFT
@@ -70,6 +71,24 @@ struct FrameParams {
     uint32_t ileave;        // > 1: frames interleaved along grid x (batch_block), else grid y = frame
 };
 
+// Pipelined reference frame (rv_render_frames with a per-frame GI update,
+// C3-C5): one launch runs the GI update of frame k+1 (reads gi_prev, writes
+// gi_next), the pre-pass of frame k+1 (into pp_hdist/pp_hshadow) and the
+// render of frame k (FrameParams), three independent parts whose latency-
+// bound waves share the machine instead of leaving it idle in three tails.
+// part[i] (0 GI, 1 pre-pass, 2 render) is dispatched i-th, over len[i]
+// workgroups of one wave (multiples of 8, so a part's XCD mapping holds).
+enum { PIPE_GI = 0, PIPE_PP = 1, PIPE_RENDER = 2 };
+struct PipeParams {
+    const uint32_t* gi_prev; uint32_t* gi_next;
+    uint64_t gi_first, gi_count;
+    uint32_t gi_frame;
+    uint32_t part[3], len[3];
+    float* pp_hdist; float* pp_hshadow;
+    unsigned long long* pp_counters;
+    unsigned long long* gi_counters;
+};
+
 struct RvHitDev {   // == rv_hit
     float pos[3], normal[3], u, v;
     int hit, undef, sphere, dda, check, pad;
@@ -84,11 +103,15 @@ void launch_csdf_import(hipStream_t s, const uint8_t* canon, uint32_t* brick, co
 void launch_csdf_export(hipStream_t s, const uint32_t* brick, uint8_t* canon, const World& w);
 void launch_gi_init(hipStream_t s, uint32_t* gi, const World& w, f3 sun, unsigned long long* counters);
 void launch_gi_update(hipStream_t s, const uint32_t* prev, uint32_t* next, const World& w, f3 sun,
-                      uint32_t frame, uint64_t first, uint64_t count, unsigned long long* counters);
+                      uint32_t frame, uint64_t first, uint64_t count, unsigned long long* counters,
+                      bool stats = false);
 // workgroups of the kernel that fills queue q (sizes its per-XCD sub-queues)
 uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
+// workgroups of each part of a pipelined launch; then the launch itself
+uint32_t pipe_len(const FrameParams& f, int part, uint64_t gi_count);
+void launch_ref_pipe(hipStream_t s, const World& w, const FrameParams& f, const PipeParams& p);
 // SCHED_COST: sort n costs (order has npad >= n entries) into a descending
 // order, clearing the costs
 void launch_chunk_order(hipStream_t s, uint32_t* cost, int* order, uint32_t n, uint32_t npad);
@@ -105,8 +128,10 @@ void launch_wf_cones(hipStream_t s, const World& w, const FrameParams& f);
 void launch_wf_shade(hipStream_t s, const World& w, const FrameParams& f, bool tiles);
 // Gathered buffer of a batch: rank q's B frames' slices back to back; slot i
 // of `ids` is entry i % per of rank i / per; frame b lands in color + b * bs.
+// bpp: bytes per packed pixel (4 RGBA8; 3 RGB24, alpha written as 255).
 void launch_untile(hipStream_t s, const uint32_t* tiles, const int* ids, int ntiles, int tile_px, int tiles_x,
-                   int W, int H, uint32_t* color, size_t pitch, int per = 0, int nbatch = 1, uint64_t bs = 0);
+                   int W, int H, uint32_t* color, size_t pitch, int per = 0, int nbatch = 1, uint64_t bs = 0,
+                   int bpp = 4);
 void launch_trace_rays(hipStream_t s, const World& w, const float* org, const float* dir, const float* dist,
                        int64_t n, RvHitDev* out);
 

@@ -146,6 +146,14 @@ class StateRender:
     def set_gi_async(self, on):
         self._check(self._L.rv_set_gi_async(self._h, int(bool(on))), "rv_set_gi_async")
 
+    def set_pipeline(self, on):
+        """rv_set_pipeline: pipelined reference frames in render_frames."""
+        self._check(self._L.rv_set_pipeline(self._h, int(bool(on))), "rv_set_pipeline")
+
+    def set_gi_stats(self, on):
+        """rv_set_gi_stats: count the GI update's traversal steps (stage 'gi')."""
+        self._check(self._L.rv_set_gi_stats(self._h, int(bool(on))), "rv_set_gi_stats")
+
     def sync(self):
         self._check(self._L.rv_sync(self._h), "rv_sync")
 

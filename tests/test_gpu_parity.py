@@ -383,14 +383,14 @@ def test_frames_in_flight_identical(rv, atlas, flags):
     hip.close()
 
 
-@pytest.mark.parametrize("flags", [8, 7])
-def test_render_frames_native_loop(rv, atlas, flags):
+@pytest.mark.parametrize("flags,T", [(8, 16), (8, 64), (7, 32)])
+def test_render_frames_native_loop(rv, atlas, flags, T):
     """rv_render_frames: the native loop over 3 frame slots equals frames
     rendered one at a time -- whole frames, a one-rank tile shard assembled
     locally, and the same shard gathered through a one-rank RCCL
     communicator (the multi-GPU code path with no peers)."""
     from rvgrt_amd.configs import TEST_POSES_128
-    lg, W, H, T = 7, 320, 192, 64
+    lg, W, H = 7, 320, 192
     gi = bool(flags & rv.RV_F_GI)
     ref = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
     cam, vp = rv.camera_from_pose(*TEST_POSES_128["P1"], W, H)
@@ -418,3 +418,66 @@ def test_render_frames_native_loop(rv, atlas, flags):
     comm.close()
     r.close()
     ref.close()
+
+
+@pytest.mark.parametrize("order", ["012", "210", "102"])
+def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order):
+    """rv_set_pipeline: render k | GI update k+1 | pre-pass k+1 in one launch.
+    The frames and the GI grid equal UpdateGIData + drawCUDA one frame at a
+    time, for every dispatch order of the parts, over a rolling GI window
+    that wraps (5000-cell windows of a 32^3 grid) -- and the oracle agrees on
+    the grid (bit-exact) and the last frame."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    monkeypatch.setenv("RV_PIPE_ORDER", order)
+    lg, W, H, rays = 7, 320, 192, 5000
+    flags = rv.RV_FLAGS_REFERENCE
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
+
+    def make():
+        r = rv.StateRender((lg, lg, lg), W, H, flags=flags, atlas=atlas, gi_rays_per_frame=rays)
+        r.world_build()
+        r.gi_update(0)
+        return r
+    ref, r = make(), make()
+    ref.set_pipeline(0)
+    for n in (1, 2, 5, 3):   # 11 frames: 2 wraps of the 32768-cell grid
+        r.render_frames(n, cam, vp, gi_per_frame=True)
+        for _ in range(n):
+            ref.update_gi_data()
+            ref.frame(cam, vp)
+        assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref.readback(rv.RV_IMAGE_COLOR)), n
+        assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref.readback(rv.RV_IMAGE_DEPTH)), n
+        assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ref.world_export(rv.RV_WORLD_GI)), n
+    # the oracle: same updates (frame numbers 0.., rolling window), same last frame
+    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas).build(gi_sweeps=1)
+    ngi, off = (1 << (lg - 2)) ** 3, 0
+    for fno in range(11):
+        ow.gi_update(fno, first=off, count=min(rays, ngi - off))
+        off = 0 if off + rays >= ngi else off + rays
+    assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi)
+    ref_img = oracle.render(ow, oracle.make_frame(W, H, flags, rv.camera_dict(cam, vp)))["rgba"]
+    d = np.abs(r.readback(rv.RV_IMAGE_COLOR).astype(np.int32) - ref_img.astype(np.int32))
+    assert d.max() <= 2 and (d.max(axis=2) == 0).mean() >= 0.995
+    assert np.array_equal(r.readback(rv.RV_IMAGE_HALF_DIST), ref.readback(rv.RV_IMAGE_HALF_DIST))
+    r.close()
+    ref.close()
+
+
+def test_pipelined_frames_stats(rv, atlas):
+    """A pipelined launch with RV_F_STATS counts its three parts into their
+    own stage blocks: the render's traces equal a one-at-a-time frame's."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H = 7, 160, 96
+    flags = rv.RV_FLAGS_REFERENCE | rv.RV_F_STATS
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
+    r = _gpu_world(rv, atlas, lg, lg, lg, W, H)
+    r.stats_reset()
+    r.frame(cam, vp, flags=flags)
+    one = {k: r.stats(k) for k in range(8)}
+    r.stats_reset()
+    r.render_frames(3, cam, vp, flags=flags, gi_per_frame=True)
+    three = {k: r.stats(k) for k in range(8)}
+    assert three[2]["traces"] == 3 * one[2]["traces"]          # render: 3 frames
+    assert three[0]["traces"] == 3 * one[0]["traces"]          # pre-pass: frame 0 + two pipelined
+    assert three[7]["gi_traces"] > 0
+    r.close()

@@ -18,7 +18,7 @@ run() {  # name limit cmd...
 for step in "$@"; do
     case $step in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
-        tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider
+        tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ${TESTS_K:+-k "$TESTS_K"}
                rc=$?; [ $rc -le 1 ] || exit 3 ;;
         bench) run bench 600 python bench.py || exit 3 ;;
         bench_c3) run bench_c3 600 python bench.py --config c3 --cpu-seconds 5 || exit 3 ;;
@@ -34,6 +34,9 @@ for step in "$@"; do
                  run pmc_$tag 600 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/pmc_$tag \
                      -o run -- python3 bench.py --steps 16 --warmup 8 --cpu-seconds 0 ${BENCH_ARGS} || exit 3
              done ;;
+        pipe) RUNS=${PIPE_RUNS:-"c3:1:012 c3:0:- c4:1:012 c4:0:- c5:1:012"} run pipe 900 tools/exp_pipe.sh || exit 3 ;;
+        shard) run shard 300 python tools/shard_probe.py c2 16 16,32,64 || exit 3 ;;
+        shard_c4) run shard_c4 300 python tools/shard_probe.py c4 1 32,64 || exit 3 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Per-rank render time of the screen-tile shard, measured on ONE GPU.
+
+For every N and tile size, renders the share of each rank r < N with the
+native loop (rv_render_frames, K frames per launch, no gather) and reports
+the slowest rank's time per frame next to the whole frame's: the render-side
+bound of the N-GPU strong scaling (the gather to rank 0 comes on top).  Used
+to choose the shard tile size; not part of the product.
+
+usage: python tools/shard_probe.py [config] [K] [tile sizes, e.g. 16,32,64]
+"""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def per_frame_us(r, cam, vp, frames, reps=3):
+    r.render_frames(frames, cam, vp)      # warm: tile lists, cost order
+    r.sync()
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r.render_frames(frames, cam, vp)
+        r.sync()
+        best = min(best, (time.perf_counter() - t0) / frames * 1e6)
+    return best
+
+
+def main():
+    import rvgrt_amd as rv
+    from rvgrt_amd.atlas import load_atlas
+    from rvgrt_amd.configs import CONFIGS, pose_f32
+
+    cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    sizes = [int(t) for t in (sys.argv[3] if len(sys.argv) > 3 else "16,32,64").split(",")]
+    torch.cuda.set_device(0)
+    W, H = cfg.width, cfg.height
+    r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=load_atlas())
+    r.world_build()
+    for s in range(max(cfg.gi_sweeps, 0)):
+        r.gi_update(s)
+    r.sync()
+    pos, yaw, pitch = pose_f32(cfg)
+    cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
+    frames = 4 * K
+    r.set_frames_in_flight(K)
+    r.set_tile_shard(64, 0, 0)
+    full = per_frame_us(r, cam, vp, frames)
+    print(f"{cfg.name}: whole frame {full:.1f} us/frame at K={K}", flush=True)
+    for T in sizes:
+        for N in (2, 4, 8):
+            t = []
+            for rank in range(N):
+                r.set_tile_shard(T, rank, N)
+                t.append(per_frame_us(r, cam, vp, frames))
+            mx = max(t)
+            print(f"  tile {T:2d} N={N}: slowest rank {mx:7.1f} us/frame, mean {sum(t) / N:7.1f}, "
+                  f"render-bound speedup {full / mx:5.2f}x  ranks: " + " ".join(f"{v:.0f}" for v in t), flush=True)
+    r.set_tile_shard(64, 0, 0)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
