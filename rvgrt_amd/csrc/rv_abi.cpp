@@ -119,6 +119,12 @@ struct rv_ctx {
     uint32_t pipe_order = 0x012;  // RV_PIPE_ORDER: dispatch order of the parts, hex digits PIPE_* (first = high)
     float* pipe_half[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [k & 1] {dist, shadow}
     bool gi_stats = false;        // rv_set_gi_stats
+    // pipelined tile loop: packed tiles / rank-0 gather buffers per frame parity, GI shard staging
+    uint32_t* pipe_tbuf[2] = {nullptr, nullptr}; uint32_t* pipe_gbuf[2] = {nullptr, nullptr};
+    size_t pipe_slice = 0, pipe_gbytes = 0;
+    uint32_t* pipe_gi_stage = nullptr; uint32_t* pipe_gi_all = nullptr;
+    uint64_t pipe_chunk = 0; int pipe_chunk_n = 0;
+    hipEvent_t pipe_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // rendered, all-gathered, gathered[2]
     int gather_bpp = 3;           // RV_GATHER_BPP: packed pixel bytes of rv_render_frames' tile gather (3 or 4)
     uint32_t frames_since_order = 0;
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
@@ -368,6 +374,9 @@ void rv_destroy(rv_ctx* c) {
     hipDeviceSynchronize();   // every frame slot's stream
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
     for (auto& ph : c->pipe_half) { hipFree(ph[0]); hipFree(ph[1]); }
+    for (int q = 0; q < 2; q++) { hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]); }
+    hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);
+    for (hipEvent_t e : c->pipe_ev) if (e) hipEventDestroy(e);
     if (!c->slots.empty()) slot_save(c);
     for (FrameSlot& sl : c->slots) slot_free(sl);
     hipFree(c->counters);
@@ -1195,6 +1204,7 @@ struct RcclApi {
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
@@ -1216,11 +1226,12 @@ bool rccl_load(const char* path, std::string& err) {
     g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))sym("ncclCommDestroy");
     g_rccl.send = (decltype(g_rccl.send))sym("ncclSend");
     g_rccl.recv = (decltype(g_rccl.recv))sym("ncclRecv");
+    g_rccl.all_gather = (decltype(g_rccl.all_gather))sym("ncclAllGather");
     g_rccl.group_start = (decltype(g_rccl.group_start))sym("ncclGroupStart");
     g_rccl.group_end = (decltype(g_rccl.group_end))sym("ncclGroupEnd");
     g_rccl.error_string = (decltype(g_rccl.error_string))sym("ncclGetErrorString");
     if (!g_rccl.get_unique_id || !g_rccl.comm_init_rank || !g_rccl.comm_destroy || !g_rccl.send || !g_rccl.recv ||
-        !g_rccl.group_start || !g_rccl.group_end || !g_rccl.error_string) {
+        !g_rccl.all_gather || !g_rccl.group_start || !g_rccl.group_end || !g_rccl.error_string) {
         err = "librccl lacks a required symbol";
         g_rccl = RcclApi{};
         return false;
@@ -1339,19 +1350,66 @@ static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* ca
 //   then      copy-back of update k+1's cells: in stream order after render
 //             k, the last reader of grid k, and before render k+1.
 // The half-res images alternate between two pairs (frame k & 1).
+// With a tile shard and a communicator of N ranks, the launch renders
+// this rank's tiles, the pre-pass covers their footprints, and the GI part
+// computes this rank's 1/N of the update's cells; an RCCL all-gather of the
+// cells (1 MiB per frame at RAYPS) on the comm stream precedes the copy-back,
+// then the packed tiles of frame k go to rank 0 on the same stream while
+// frame k+1 renders; rank 0 assembles frame k after launching frame k+1.
+// Without a communicator an N > 1 shard renders its share only (its GI part
+// covers the whole window, so its grid stays the reference's).
 static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
-                                const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S) {
+                                const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S,
+                                rv_comm* comm) {
     const int W = c->cfg.width, H = c->cfg.height;
     const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
+    const int N = tiles ? c->shard_n : 1, R = tiles ? c->shard_rank : 0, T = c->shard_px;
+    const bool xchg = tiles && comm;   // GI shard + all-gather, tile gather to rank 0 (also for one rank)
+    // timing probe (env RV_GI_SHARD_PROBE, no communicator): this rank's GI share only, no exchange --
+    // the grid is then NOT the reference's; only for sizing the multi-GPU loop on one GPU
+    const bool probe = tiles && !comm && N > 1 && getenv("RV_GI_SHARD_PROBE") != nullptr;
+    const bool shard_gi = xchg || probe;
+    const int bpp = c->gather_bpp;
+    const size_t slice = tiles ? (size_t)c->shard_max * T * T * bpp : 0;
+    const uint64_t n = n_gi(c), rays = c->cfg.gi_rays_per_frame;
+    const uint64_t chunk = shard_gi ? (rays + N - 1) / N : 0;   // GI cells per rank (all-gather unit)
     for (auto& ph : c->pipe_half)
         for (int q = 0; q < 2; q++)
             if (!ph[q]) HIP_TRY(c, hipMalloc(&ph[q], hbytes));
     if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
+    if (tiles && (c->pipe_slice != slice || c->pipe_gbytes != (root ? slice * N : 0))) {
+        HIP_TRY(c, hipDeviceSynchronize());
+        for (int q = 0; q < 2; q++) {
+            hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]);
+            c->pipe_tbuf[q] = nullptr; c->pipe_gbuf[q] = nullptr;
+            HIP_TRY(c, hipMalloc(&c->pipe_tbuf[q], slice ? slice : 1));
+            if (root) HIP_TRY(c, hipMalloc(&c->pipe_gbuf[q], slice * N));
+        }
+        c->pipe_slice = slice; c->pipe_gbytes = root ? slice * N : 0;
+    }
+    if (shard_gi && (c->pipe_chunk != chunk || c->pipe_chunk_n != N)) {
+        HIP_TRY(c, hipDeviceSynchronize());
+        hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);
+        c->pipe_gi_stage = nullptr; c->pipe_gi_all = nullptr;
+        HIP_TRY(c, hipMalloc(&c->pipe_gi_stage, chunk * 4));
+        HIP_TRY(c, hipMalloc(&c->pipe_gi_all, chunk * N * 4));
+        c->pipe_chunk = chunk; c->pipe_chunk_n = N;
+    }
+    for (hipEvent_t& e : c->pipe_ev)
+        if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     slot_save(c);
     slot_load(c, 0);
     c->stream = S;
     if (rv_status ws = wait_all_frames(c)) return ws;   // frames of earlier calls, the last world write
-    const uint64_t n = n_gi(c), rays = c->cfg.gi_rays_per_frame;
+    if (xchg) {   // the comm stream starts after the frames of earlier calls too
+        HIP_TRY(c, hipEventRecord(c->pipe_ev[0], S));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->pipe_ev[0], 0));
+    }
+    if (tiles) {
+        if (rv_status us = upload_ids(c, c->untile_ids, c->shard_all.data(), (int)c->shard_all.size(), nullptr)) return us;
+        if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
+    }
     auto next_range = [&](uint32_t& fr, uint64_t& first, uint64_t& count) {   // rv_update_gi_data's walk
         fr = c->gi_frame;
         first = c->gi_offset;
@@ -1360,11 +1418,17 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         if (c->gi_offset + rays >= n) c->gi_offset = 0;   // src/CoarseArray.cu:392-394
         else c->gi_offset += rays;
     };
+    auto tile_params = [&](FrameParams& f, int k) {
+        if (!tiles) return;
+        f.tiles = c->tiles.d; f.ntiles = (int)c->shard_ids.size(); f.tile_px = T; f.tiles_x = (W + T - 1) / T;
+        f.tilebuf = c->pipe_tbuf[k & 1]; f.tile_bpp = bpp;
+        f.chunk_order[CG_RENDER] = c->tile_order; f.chunk_cost[CG_RENDER] = c->tile_cost;
+    };
     const World w = current_world(c);
     unsigned long long* cnt_gi = c->counters + (size_t)ST_GI * NCNT;
     uint32_t fr = 0;
     uint64_t first = 0, count = 0;
-    next_range(fr, first, count);
+    next_range(fr, first, count);   // frame 0's update: every rank the whole window (identical grids)
     launch_gi_update(S, c->gi, c->gi_tmp, w, sun_dir(), fr, first, count, cnt_gi, c->gi_stats);
     LAUNCH_CHECK(c);
     HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
@@ -1372,22 +1436,43 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
         f.hdist = c->pipe_half[0][0]; f.hshadow = c->pipe_half[0][1];
         f.counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
-        launch_prepass(S, w, f);
+        tile_params(f, 0);
+        if (tiles) launch_prepass_tiles(S, w, f); else launch_prepass(S, w, f);
         LAUNCH_CHECK(c);
     }
+    const int tiles_x = (W + T - 1) / std::max(T, 1);
+    auto untile = [&](int k) -> rv_status {   // rank 0: assemble frame k once its gather is done
+        HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[2 + (k & 1)], 0));
+        launch_untile(S, c->pipe_gbuf[k & 1], c->untile_ids.d, (int)c->shard_all.size(), T, tiles_x, W, H, c->color,
+                      c->color_pitch, c->shard_max, 1, 0, bpp);
+        LAUNCH_CHECK(c);
+        return RV_OK;
+    };
     for (int k = 0; k < frames; k++) {
         const bool more = k + 1 < frames;
         FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
         f.hdist = c->pipe_half[k & 1][0]; f.hshadow = c->pipe_half[k & 1][1];
         f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
+        tile_params(f, k);
+        if (xchg && k >= 2)   // tile buffer k & 1 is free once frame k-2's gather has read it
+            HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[2 + (k & 1)], 0));
         PipeParams p{};
-        p.gi_prev = c->gi; p.gi_next = c->gi_tmp;
-        if (more) next_range(p.gi_frame, first, count);
-        p.gi_first = first; p.gi_count = more ? count : 0;
+        p.gi_prev = c->gi;
+        uint64_t mine = 0, mfirst = 0;
+        if (more) {
+            next_range(p.gi_frame, first, count);
+            mfirst = first; mine = count;
+            if (shard_gi) {
+                mfirst = first + std::min<uint64_t>(count, (uint64_t)R * chunk);
+                mine = std::min<uint64_t>(chunk, first + count - mfirst);
+            }
+        }
+        p.gi_first = mfirst; p.gi_count = mine;
+        p.gi_next = shard_gi ? c->pipe_gi_stage : c->gi_tmp + first;
         p.pp_hdist = c->pipe_half[(k + 1) & 1][0]; p.pp_hshadow = c->pipe_half[(k + 1) & 1][1];
         p.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
         p.gi_counters = cnt_gi;
-        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, count) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
+        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, mine) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
                                   pipe_len(f, PIPE_RENDER, 0)};
         for (int i = 0; i < 3; i++) {
             p.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;
@@ -1405,17 +1490,60 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
             c->ev_used[c->timing_n] = 2;
             c->timing_n++;
         }
-        if (more)
-            HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+        if (xchg) {
+            HIP_TRY(c, hipEventRecord(c->pipe_ev[0], S));   // frame k rendered, shard k+1 computed
+            HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->pipe_ev[0], 0));
+            if (more) {   // the update's cells from every rank, then the copy-back on S
+                NCCL_TRY(c, g_rccl.all_gather(c->pipe_gi_stage, c->pipe_gi_all, chunk, ncclUint32, comm->comm,
+                                              c->comm_stream));
+                HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
+                HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[1], 0));
+                HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->pipe_gi_all, count * 4, hipMemcpyDeviceToDevice, S));
+            }
+            // frame k's packed tiles to rank 0, after the all-gather on the comm stream
+            if (root)
+                HIP_TRY(c, hipMemcpyAsync(c->pipe_gbuf[k & 1], c->pipe_tbuf[k & 1], slice, hipMemcpyDeviceToDevice,
+                                          c->comm_stream));
+            NCCL_TRY(c, g_rccl.group_start());
+            if (root) {
+                for (int q = 1; q < N; q++)
+                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(c->pipe_gbuf[k & 1]) + (size_t)q * slice, slice,
+                                            ncclUint8, q, comm->comm, c->comm_stream));
+            } else {
+                NCCL_TRY(c, g_rccl.send(c->pipe_tbuf[k & 1], slice, ncclUint8, 0, comm->comm, c->comm_stream));
+            }
+            NCCL_TRY(c, g_rccl.group_end());
+            HIP_TRY(c, hipEventRecord(c->pipe_ev[2 + (k & 1)], c->comm_stream));
+            if (root && k >= 1)   // frame k-1, whose gather overlapped this launch
+                if (rv_status us = untile(k - 1)) return us;
+        } else {
+            if (more && !probe)
+                HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+            if (tiles && N == 1) {   // one rank: assemble locally
+                launch_untile(S, c->pipe_tbuf[k & 1], c->untile_ids.d, (int)c->shard_all.size(), T, tiles_x, W, H,
+                              c->color, c->color_pitch, c->shard_max, 1, 0, bpp);
+                LAUNCH_CHECK(c);
+            }
+        }
         if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
             c->frames_since_order = 0;
-            launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                               n_chunks_pad(f.hw, f.hh));
-            launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
-                               n_chunks_pad(f.W, f.H));
+            if (tiles) {
+                launch_chunk_order(S, c->tile_cost, c->tile_order, (uint32_t)f.ntiles, ((uint32_t)f.ntiles + 7u) & ~7u);
+            } else {
+                launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
+                                   n_chunks_pad(f.hw, f.hh));
+                launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
+                                   n_chunks_pad(f.W, f.H));
+            }
             LAUNCH_CHECK(c);
         }
         c->frame_seq++;
+    }
+    if (xchg) {
+        if (root)
+            if (rv_status us = untile(frames - 1)) return us;
+        HIP_TRY(c, hipEventRecord(c->pipe_ev[0], c->comm_stream));   // S sees the last gather done
+        HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[0], 0));
     }
     // the last frame's half-res images become the slot's (rv_readback)
     const int lk = (frames - 1) & 1;
@@ -1678,9 +1806,9 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
         c->stream = caller;
         return st;
     }
-    if (gi_per_frame && (flags & RV_F_PREPASS) && !tiles && c->pipe && c->megakernel && frames > 0) {
+    if (gi_per_frame && (flags & RV_F_PREPASS) && c->pipe && c->megakernel && frames > 0) {
         hipStream_t S = own0 ? c->fstreams[0] : caller;
-        st = render_gi_pipe(c, frames, cam, vp16, pvp16, time, jx, jy, flags, S);
+        st = render_gi_pipe(c, frames, cam, vp16, pvp16, time, jx, jy, flags, S, comm);
         c->stream = caller;
         if (st != RV_OK) return st;
         if (S != caller) HIP_TRY(c, hipStreamWaitEvent(caller, c->slots[0].done, 0));

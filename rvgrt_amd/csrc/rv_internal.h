@@ -73,9 +73,12 @@ struct FrameParams {
 
 // Pipelined reference frame (rv_render_frames with a per-frame GI update,
 // C3-C5): one launch runs the GI update of frame k+1 (reads gi_prev, writes
-// gi_next), the pre-pass of frame k+1 (into pp_hdist/pp_hshadow) and the
-// render of frame k (FrameParams), three independent parts whose latency-
-// bound waves share the machine instead of leaving it idle in three tails.
+// cell gi_first + i to gi_next[i]), the pre-pass of frame k+1 (into
+// pp_hdist/pp_hshadow) and the render of frame k (FrameParams), three
+// independent parts whose latency-bound waves share the machine instead of
+// leaving it idle in three tails.  With a tile shard (FrameParams::tiles) the
+// pre-pass covers the tiles' half-res footprints and the render packs the
+// tiles, and the GI part is this rank's share of the update's cells.
 // part[i] (0 GI, 1 pre-pass, 2 render) is dispatched i-th, over len[i]
 // workgroups of one wave (multiples of 8, so a part's XCD mapping holds).
 enum { PIPE_GI = 0, PIPE_PP = 1, PIPE_RENDER = 2 };

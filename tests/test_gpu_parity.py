@@ -383,7 +383,7 @@ def test_frames_in_flight_identical(rv, atlas, flags):
     hip.close()
 
 
-@pytest.mark.parametrize("flags,T", [(8, 16), (8, 64), (7, 32)])
+@pytest.mark.parametrize("flags,T", [(8, 16), (8, 64), (7, 32), (7, 16)])
 def test_render_frames_native_loop(rv, atlas, flags, T):
     """rv_render_frames: the native loop over 3 frame slots equals frames
     rendered one at a time -- whole frames, a one-rank tile shard assembled

@@ -37,6 +37,7 @@ for step in "$@"; do
         pipe) RUNS=${PIPE_RUNS:-"c3:1:012 c3:0:- c4:1:012 c4:0:- c5:1:012"} run pipe 900 tools/exp_pipe.sh || exit 3 ;;
         shard) run shard 300 python tools/shard_probe.py c2 16 16,32,64 || exit 3 ;;
         shard_c4) run shard_c4 300 python tools/shard_probe.py c4 1 32,64 || exit 3 ;;
+        shard_gi) RV_GI_SHARD_PROBE=1 run shard_gi 600 python tools/shard_probe.py ${SHARD_CFG:-c4} 1 ${SHARD_T:-16,32} || exit 3 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -19,13 +19,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def per_frame_us(r, cam, vp, frames, reps=3):
-    r.render_frames(frames, cam, vp)      # warm: tile lists, cost order
+def per_frame_us(r, cam, vp, frames, gi, reps=3):
+    r.render_frames(frames, cam, vp, gi_per_frame=gi)      # warm: tile lists, cost order
     r.sync()
     best = 1e30
     for _ in range(reps):
         t0 = time.perf_counter()
-        r.render_frames(frames, cam, vp)
+        r.render_frames(frames, cam, vp, gi_per_frame=gi)
         r.sync()
         best = min(best, (time.perf_counter() - t0) / frames * 1e6)
     return best
@@ -48,20 +48,39 @@ def main():
     r.sync()
     pos, yaw, pitch = pose_f32(cfg)
     cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
-    frames = 4 * K
+    frames = max(4 * K, 32)   # the pipelined GI loop's prologue amortised over the call
     r.set_frames_in_flight(K)
     r.set_tile_shard(64, 0, 0)
-    full = per_frame_us(r, cam, vp, frames)
+    gi = cfg.gi_per_frame
+    full = per_frame_us(r, cam, vp, frames, gi)
     print(f"{cfg.name}: whole frame {full:.1f} us/frame at K={K}", flush=True)
     for T in sizes:
         for N in (2, 4, 8):
             t = []
             for rank in range(N):
                 r.set_tile_shard(T, rank, N)
-                t.append(per_frame_us(r, cam, vp, frames))
+                t.append(per_frame_us(r, cam, vp, frames, gi))
             mx = max(t)
             print(f"  tile {T:2d} N={N}: slowest rank {mx:7.1f} us/frame, mean {sum(t) / N:7.1f}, "
                   f"render-bound speedup {full / mx:5.2f}x  ranks: " + " ".join(f"{v:.0f}" for v in t), flush=True)
+    if gi and os.environ.get("PROBE_STAGES"):
+        # one frame at a time (no pipelining): stand-alone launch time of each stage for
+        # rank 0's share -- which part's longest wave bounds a pipelined launch
+        import rvgrt_amd._lib as L
+        r.set_pipeline(0)
+        for T in sizes:
+            for N in (1, 8):
+                r.set_tile_shard(T, 0, N)
+                r.render_frames(8, cam, vp, gi_per_frame=True)
+                r.timing_enable(40)
+                r.render_frames(16, cam, vp, gi_per_frame=True)
+                r.sync()
+                ms, _ = r.timing_stages()
+                n = r.timing_launches()
+                r.timing_enable(0)
+                print(f"  stages tile {T} rank 0 of {N}: " + ", ".join(
+                    f"{k} {ms[k] / n[k] * 1e3:.0f} us" for k in L.STAGES if n[k]), flush=True)
+        r.set_pipeline(1)
     r.set_tile_shard(64, 0, 0)
     r.close()
 
