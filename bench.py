@@ -331,9 +331,9 @@ def main():
     # frames (frame slots); with a per-frame GI update only the pre-pass is
     # grouped and the render runs frame by frame.
     grouped = native and args.path == "fused" and nfl > 1
-    # pipelined reference frames: every launch is k_ref_pipe (timed as stage "primary")
-    piped = (native and args.path == "fused" and args.pipe and gi_per_frame and bool(flags & rv.RV_F_PREPASS)
-             and world_size == 1)
+    # pipelined reference frames: every launch is k_ref_pipe (timed as stage "primary"); with N > 1
+    # ranks a rank's launch holds its tiles and 1/N of the GI update's cells
+    piped = native and args.path == "fused" and args.pipe and gi_per_frame and bool(flags & rv.RV_F_PREPASS)
     gi_groups = grouped and gi_per_frame and bool(flags & rv.RV_F_PREPASS) and world_size == 1 and not piped
     fpl = nfl if (grouped and not gi_per_frame) else 1
     stage_fpl = {name: fpl for name in rv._lib.STAGES}
