@@ -31,6 +31,7 @@ for step in "$@"; do
              IFS=';' read -ra SETS <<< "$sets"
              for ctr in "${SETS[@]}"; do
                  tag=$(echo $ctr | tr ' ' '_' | cut -c1-60)
+                 tag=${PMC_TAG:-}$tag
                  run pmc_$tag 600 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/pmc_$tag \
                      -o run -- python3 bench.py --steps 16 --warmup 8 --cpu-seconds 0 ${BENCH_ARGS} || exit 3
              done ;;

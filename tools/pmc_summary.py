@@ -29,9 +29,10 @@ def main():
     ap.add_argument("--kernel", default="k_render<false")
     ap.add_argument("--out", default=None)
     ap.add_argument("--fpl", type=int, default=8, help="frames per launch of the profiled bench run")
+    ap.add_argument("--prefix", default="", help="pass directories pmc_<prefix>* only (gpu_run.sh PMC_TAG)")
     a = ap.parse_args()
     vals = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(a.dir, "pmc_*", "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(a.dir, f"pmc_{a.prefix}*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
             if a.kernel not in name:
