@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>   // types only: RCCL is resolved at run time (rccl_load)
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -125,6 +126,9 @@ struct rv_ctx {
     uint32_t* pipe_gi_stage = nullptr; uint32_t* pipe_gi_all = nullptr;
     uint64_t pipe_chunk = 0; int pipe_chunk_n = 0;
     hipEvent_t pipe_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // rendered, all-gathered, gathered[2]
+    uint32_t* pipe_wstat = nullptr;   // env RV_PIPE_WAVE_STATS: per-wave records of the first launches
+    uint32_t pipe_launches = 0;
+    uint32_t pipe_wnb[64] = {};       // workgroups of each recorded launch
     int gather_bpp = 3;           // RV_GATHER_BPP: packed pixel bytes of rv_render_frames' tile gather (3 or 4)
     uint32_t frames_since_order = 0;
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
@@ -377,6 +381,30 @@ void rv_destroy(rv_ctx* c) {
     for (int q = 0; q < 2; q++) { hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]); }
     hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);
     for (hipEvent_t e : c->pipe_ev) if (e) hipEventDestroy(e);
+    if (c->pipe_wstat) {   // RV_PIPE_WAVE_STATS: per part, the longest wave and the 99th percentile per launch
+        const char* names[3] = {"gi", "prepass", "render"};
+        double mx[3] = {0, 0, 0}, p99[3] = {0, 0, 0};
+        uint32_t used = 0;
+        for (uint32_t i = 4; i < c->pipe_launches; i++, used++) {   // the first launches warm the cost order
+            std::vector<uint32_t> h(c->pipe_wnb[i]);
+            if (hipMemcpy(h.data(), c->pipe_wstat + (size_t)i * (1u << 18), h.size() * 4, hipMemcpyDeviceToHost) !=
+                hipSuccess)
+                break;
+            for (int q = 0; q < 3; q++) {
+                std::vector<uint32_t> v;
+                for (uint32_t r : h)
+                    if (r != 0xFFFFFFFFu && (r >> 30) == (uint32_t)q) v.push_back(r & 0x3FFFFFFFu);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                mx[q] += v.back();
+                p99[q] += v[(size_t)(0.99 * (double)(v.size() - 1))];
+            }
+        }
+        for (int q = 0; used && q < 3; q++)
+            fprintf(stderr, "[rvgrt] pipe waves %-8s longest %7.1f us  p99 %7.1f us  (mean over %u launches)\n",
+                    names[q], mx[q] / used / 100.0, p99[q] / used / 100.0, used);
+        hipFree(c->pipe_wstat);
+    }
     if (!c->slots.empty()) slot_save(c);
     for (FrameSlot& sl : c->slots) slot_free(sl);
     hipFree(c->counters);
@@ -1358,6 +1386,8 @@ static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* ca
 // frame k+1 renders; rank 0 assembles frame k after launching frame k+1.
 // Without a communicator an N > 1 shard renders its share only (its GI part
 // covers the whole window, so its grid stays the reference's).
+constexpr uint32_t PIPE_WSTAT_N = 32, PIPE_WSTAT_MAXB = 1u << 18;   // launches, workgroups per launch
+
 static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
                                 const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S,
                                 rv_comm* comm) {
@@ -1477,6 +1507,15 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         for (int i = 0; i < 3; i++) {
             p.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;
             p.len[i] = lens[p.part[i]];
+        }
+        if (getenv("RV_PIPE_WAVE_STATS") && more) {   // diagnostics: summarised by rv_destroy
+            const uint32_t nb = p.len[0] + p.len[1] + p.len[2];
+            if (!c->pipe_wstat) HIP_TRY(c, hipMalloc(&c->pipe_wstat, (size_t)PIPE_WSTAT_N * PIPE_WSTAT_MAXB * 4));
+            if (c->pipe_launches < PIPE_WSTAT_N && nb <= PIPE_WSTAT_MAXB) {
+                p.wave_max = c->pipe_wstat + (size_t)c->pipe_launches * PIPE_WSTAT_MAXB;
+                HIP_TRY(c, hipMemsetAsync(p.wave_max, 0xFF, (size_t)nb * 4, S));
+                c->pipe_wnb[c->pipe_launches++] = nb;
+            }
         }
         // timing (rv_timing_stages: stage ST_PRIMARY) records the full launches
         const bool timed = (more || frames == 1) && c->timing_n < c->timing_cap;

@@ -90,6 +90,7 @@ struct PipeParams {
     float* pp_hdist; float* pp_hshadow;
     unsigned long long* pp_counters;
     unsigned long long* gi_counters;
+    uint32_t* wave_max;     // diagnostics (env RV_PIPE_WAVE_STATS): per workgroup, part << 30 | 10-ns ticks
 };
 
 struct RvHitDev {   // == rv_hit

@@ -36,6 +36,12 @@ for step in "$@"; do
                      -o run -- python3 bench.py --steps 16 --warmup 8 --cpu-seconds 0 ${BENCH_ARGS} || exit 3
              done ;;
         pipe) RUNS=${PIPE_RUNS:-"c3:1:012 c3:0:- c4:1:012 c4:0:- c5:1:012"} run pipe 900 tools/exp_pipe.sh || exit 3 ;;
+        waves) # PW_RUNS="c3:0 c5:8:32 ..." (config:nranks[:tile_px])
+               for pw in ${PW_RUNS:-c3:0 c4:0 c5:0 c4:4:32 c5:8:32}; do
+                   IFS=: read -r pc pn pt <<< "$pw"
+                   RV_PIPE_WAVE_STATS=1 RV_GI_SHARD_PROBE=1 run waves_${pc}_${pn} 300 python tools/pipe_waves.py $pc $pn ${pt:-32} || exit 3
+                   grep -h "us/frame\|longest" gpurun_out/waves_${pc}_${pn}.log
+               done ;;
         shard) run shard 300 python tools/shard_probe.py c2 16 16,32,64 || exit 3 ;;
         shard_c4) run shard_c4 300 python tools/shard_probe.py c4 1 32,64 || exit 3 ;;
         shard_gi) RV_GI_SHARD_PROBE=1 run shard_gi 600 python tools/shard_probe.py ${SHARD_CFG:-c4} 1 ${SHARD_T:-16,32} || exit 3 ;;
