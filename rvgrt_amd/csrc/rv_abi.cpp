@@ -1386,6 +1386,9 @@ static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* ca
 // frame k+1 renders; rank 0 assembles frame k after launching frame k+1.
 // Without a communicator an N > 1 shard renders its share only (its GI part
 // covers the whole window, so its grid stays the reference's).
+#ifndef RV_PIPE_DIAG
+#define RV_PIPE_DIAG 0   // per-wave diagnostics of the pipelined launch (tools/pipe_waves.py builds it)
+#endif
 constexpr uint32_t PIPE_WSTAT_N = 32, PIPE_WSTAT_MAXB = 1u << 18;   // launches, workgroups per launch
 
 static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
@@ -1508,7 +1511,7 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
             p.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;
             p.len[i] = lens[p.part[i]];
         }
-        if (getenv("RV_PIPE_WAVE_STATS") && more) {   // diagnostics: summarised by rv_destroy
+        if (RV_PIPE_DIAG && getenv("RV_PIPE_WAVE_STATS") && more) {   // diagnostics: summarised by rv_destroy
             const uint32_t nb = p.len[0] + p.len[1] + p.len[2];
             if (!c->pipe_wstat) HIP_TRY(c, hipMalloc(&c->pipe_wstat, (size_t)PIPE_WSTAT_N * PIPE_WSTAT_MAXB * 4));
             if (c->pipe_launches < PIPE_WSTAT_N && nb <= PIPE_WSTAT_MAXB) {

@@ -39,7 +39,8 @@ for step in "$@"; do
         waves) # PW_RUNS="c3:0 c5:8:32 ..." (config:nranks[:tile_px])
                for pw in ${PW_RUNS:-c3:0 c4:0 c5:0 c4:4:32 c5:8:32}; do
                    IFS=: read -r pc pn pt <<< "$pw"
-                   RV_PIPE_WAVE_STATS=1 RV_GI_SHARD_PROBE=1 run waves_${pc}_${pn} 300 python tools/pipe_waves.py $pc $pn ${pt:-32} || exit 3
+                   RVGRT_LIB=$PWD/rvgrt_amd/variants/diag/librvgrt_hip.so RV_PIPE_WAVE_STATS=1 RV_GI_SHARD_PROBE=1 \
+                       run waves_${pc}_${pn} 300 python tools/pipe_waves.py $pc $pn ${pt:-32} || exit 3
                    grep -h "us/frame\|longest" gpurun_out/waves_${pc}_${pn}.log
                done ;;
         shard) run shard 300 python tools/shard_probe.py c2 16 16,32,64 || exit 3 ;;
