@@ -81,6 +81,10 @@ def main():
                     help="screen-tile size of the N>1 shard (default: 16 px without the pre-pass, 32 with it; "
                          "tools/shard_probe.py: C2 at 8 ranks renders its slowest share in 19.6 us/frame at "
                          "16 px vs 30.9 at 64 px)")
+    ap.add_argument("--root-weight", type=float, default=None,
+                    help="N>1 native loop: rank 0's share of tiles relative to the others (rank 0 also receives "
+                         "and assembles every frame); default 1 - 0.019 (N-1): its measured assembly cost is "
+                         "1.9%% of a whole frame's render (profiles/r01_shard_probe_c2_root.log)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
@@ -228,7 +232,11 @@ def main():
         # RCCL communicator of the library (joins torch's librccl); id from rank 0.
         # Any rank that cannot load RCCL or create its side makes every rank
         # fall back to the Python loop's torch.distributed gather.
+        w0 = args.root_weight if args.root_weight is not None else 1.0 - 0.019 * (world_size - 1)
+        os.environ["RV_SHARD_ROOT_WEIGHT"] = repr(w0)   # read by rv_set_tile_shard; identical on every rank
         r.set_tile_shard(T, rank, world_size)
+        from rvgrt_amd.tiles import shard_owners
+        my_tiles = np.flatnonzero(shard_owners(W, H, T, world_size, w0) == rank).astype(np.int32)
         uid = torch.zeros(rv.Comm.ID_BYTES + 1, dtype=torch.uint8, device=dev)
         if rank == 0:
             try:
@@ -251,6 +259,7 @@ def main():
                 comm = None
             r.set_tile_shard(T, 0, 0)
             native = False
+            my_tiles = np.arange(rank, ntiles, world_size, dtype=np.int32)   # the Python loop's interleave
 
     def run_native(k):
         r.set_stream(stream.cuda_stream)
@@ -456,6 +465,7 @@ def main():
             "pipelined": bool(piped),
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,
+            "root_weight": float(os.environ.get("RV_SHARD_ROOT_WEIGHT", "1")) if world_size > 1 and native else None,
             "gather_check": gather_check,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -69,6 +69,7 @@ SIGNATURES = [
     ("rv_last_error", C.c_char_p, [P]),
     ("rv_set_stream", I32, [P, P]),
     ("rv_set_frame_path", I32, [P, I32]),
+    ("rv_tile_shard_assign", I32, [I32, I32, I32, I32, C.c_float, P]),
     ("rv_set_gi_async", I32, [P, I32]),
     ("rv_set_pipeline", I32, [P, I32]),
     ("rv_set_gi_stats", I32, [P, I32]),

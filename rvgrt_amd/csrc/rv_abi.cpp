@@ -1767,6 +1767,27 @@ void rv_comm_destroy(rv_comm* m) {
     delete m;
 }
 
+rv_status rv_tile_shard_assign(int32_t width, int32_t height, int32_t tile_px, int32_t nranks, float root_weight,
+                               int32_t* owner) {
+    if (width <= 0 || height <= 0 || tile_px <= 0 || nranks <= 0 || !owner) return RV_ERR_INVALID;
+    const int nt = ((width + tile_px - 1) / tile_px) * ((height + tile_px - 1) / tile_px);
+    const double w0 = std::min(1.0, std::max(0.05, (double)root_weight));
+    // Tiles are dealt in order to the rank with the fewest tiles per unit of weight (ties: the
+    // lowest rank): equal weights give the plain interleave t = rank, rank + nranks, ...
+    std::vector<int> cnt((size_t)nranks, 0);
+    for (int t = 0; t < nt; t++) {
+        int best = 0;
+        double bv = 0.0;
+        for (int q = 0; q < nranks; q++) {
+            const double v = (double)(cnt[(size_t)q] + 1) / (q == 0 ? w0 : 1.0);
+            if (q == 0 || v < bv) { best = q; bv = v; }
+        }
+        cnt[(size_t)best]++;
+        owner[t] = best;
+    }
+    return RV_OK;
+}
+
 rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks) {
     if (!c || nranks < 0 || (nranks > 0 && (rank < 0 || rank >= nranks))) return RV_ERR_INVALID;
     if (nranks > 0 && (tile_px < 16 || (tile_px & 15))) return fail(c, RV_ERR_INVALID, "tile_px must be a multiple of 16");
@@ -1775,13 +1796,18 @@ rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nr
     if (nranks == 0) return RV_OK;
     const int tx = (c->cfg.width + tile_px - 1) / tile_px, ty = (c->cfg.height + tile_px - 1) / tile_px;
     const int nt = tx * ty;
-    c->shard_max = (nt + nranks - 1) / nranks;
-    for (int t = rank; t < nt; t += nranks) c->shard_ids.push_back(t);   // interleaved (tiles.py rank_tiles)
+    double w0 = 1.0;
+    if (const char* e = getenv("RV_SHARD_ROOT_WEIGHT")) w0 = atof(e);
+    std::vector<int32_t> owner((size_t)nt);
+    if (rv_status as = rv_tile_shard_assign(c->cfg.width, c->cfg.height, tile_px, nranks, (float)w0, owner.data()))
+        return fail(c, as, "rv_tile_shard_assign");
+    std::vector<std::vector<int32_t>> own((size_t)nranks);
+    for (int t = 0; t < nt; t++) own[(size_t)owner[(size_t)t]].push_back(t);
+    for (const auto& o : own) c->shard_max = std::max(c->shard_max, (int)o.size());
+    c->shard_ids = own[(size_t)rank];
     c->shard_all.assign((size_t)nranks * c->shard_max, -1);              // gathered layout, -1 = padding slot
-    for (int q = 0; q < nranks; q++) {
-        int k = 0;
-        for (int t = q; t < nt; t += nranks) c->shard_all[(size_t)q * c->shard_max + k++] = t;
-    }
+    for (int q = 0; q < nranks; q++)
+        for (size_t k = 0; k < own[(size_t)q].size(); k++) c->shard_all[(size_t)q * c->shard_max + k] = own[(size_t)q][k];
     return RV_OK;
 }
 

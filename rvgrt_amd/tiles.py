@@ -24,6 +24,21 @@ def rank_tiles(ntiles: int, rank: int, world_size: int) -> np.ndarray:
     return np.arange(rank, ntiles, world_size, dtype=np.int32)
 
 
+def shard_owners(width: int, height: int, tile_px: int, world_size: int, root_weight: float = 1.0) -> np.ndarray:
+    """Owner rank of every tile as the native loop deals them (rv_tile_shard_assign,
+    host-only C ABI): interleaved, rank 0 weighing root_weight.  Equal weights give
+    rank_tiles' assignment."""
+    from . import _lib
+    import ctypes as C
+    nt = len(np.arange(0, ((width + tile_px - 1) // tile_px) * ((height + tile_px - 1) // tile_px)))
+    out = np.empty(nt, np.int32)
+    st = _lib.load().rv_tile_shard_assign(int(width), int(height), int(tile_px), int(world_size),
+                                          float(root_weight), out.ctypes.data_as(C.c_void_p))
+    if st != 0:
+        raise ValueError(f"rv_tile_shard_assign: status {st}")
+    return out
+
+
 def max_tiles_per_rank(ntiles: int, world_size: int) -> int:
     return (ntiles + world_size - 1) // world_size
 

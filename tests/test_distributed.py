@@ -95,3 +95,26 @@ def test_pack_untile_roundtrip():
         ids = tiles.rank_tiles(tx * ty, r, 3)
         tiles.untile(tiles.pack_tiles(img, ids, 32), ids, 32, out)
     assert np.array_equal(out, img)
+
+
+@pytest.mark.parametrize("world_size", [2, 4, 8])
+def test_weighted_shard_assignment(world_size):
+    """rv_tile_shard_assign (host-only C ABI, the native loop's deal): equal
+    weights reproduce the plain interleave; a lighter rank 0 gets about
+    root_weight times the others' tiles, still spread over the whole frame;
+    every tile has exactly one owner."""
+    from rvgrt_amd.tiles import rank_tiles, shard_owners
+    W, H, T = 1920, 1080, 16
+    own = shard_owners(W, H, T, world_size, 1.0)
+    nt = own.size
+    for r in range(world_size):
+        assert np.array_equal(np.flatnonzero(own == r), rank_tiles(nt, r, world_size))
+    w0 = 1.0 - 0.019 * (world_size - 1)
+    own = shard_owners(W, H, T, world_size, w0)
+    counts = np.bincount(own, minlength=world_size)
+    assert counts.sum() == nt and counts.min() > 0
+    others = counts[1:].mean()
+    assert abs(counts[0] / others - w0) < 0.01
+    assert counts[1:].max() - counts[1:].min() <= 1
+    gaps = np.diff(np.flatnonzero(own == 0))
+    assert gaps.max() <= 2 * world_size   # rank 0's tiles stay interleaved over the frame

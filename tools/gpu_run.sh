@@ -43,7 +43,7 @@ for step in "$@"; do
                        run waves_${pc}_${pn} 300 python tools/pipe_waves.py $pc $pn ${pt:-32} || exit 3
                    grep -h "us/frame\|longest" gpurun_out/waves_${pc}_${pn}.log
                done ;;
-        shard) run shard 300 python tools/shard_probe.py c2 16 16,32,64 || exit 3 ;;
+        shard) run shard 300 python tools/shard_probe.py c2 16 ${SHARD_T:-16,32,64} || exit 3 ;;
         shard_c4) run shard_c4 300 python tools/shard_probe.py c4 1 32,64 || exit 3 ;;
         shard_gi) RV_GI_SHARD_PROBE=1 run shard_gi 600 python tools/shard_probe.py ${SHARD_CFG:-c4} 1 ${SHARD_T:-16,32} || exit 3 ;;
         *) echo "unknown step $step"; exit 2 ;;

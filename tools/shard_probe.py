@@ -63,6 +63,29 @@ def main():
             mx = max(t)
             print(f"  tile {T:2d} N={N}: slowest rank {mx:7.1f} us/frame, mean {sum(t) / N:7.1f}, "
                   f"render-bound speedup {full / mx:5.2f}x  ranks: " + " ".join(f"{v:.0f}" for v in t), flush=True)
+    if os.environ.get("PROBE_ROOT"):
+        # rank 0's extra work at any N: the whole frame's untile (and the gather path) --
+        # one rank holding every tile, assembled locally and through a one-rank RCCL communicator
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29541")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        for T in sizes:
+            r.set_tile_shard(T, 0, 1)
+            local = per_frame_us(r, cam, vp, frames, gi)
+            comm = rv.Comm(r, rv.Comm.unique_id(), 1, 0)
+            r.render_frames(frames, cam, vp, gi_per_frame=gi, comm=comm)
+            r.sync()
+            best = 1e30
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r.render_frames(frames, cam, vp, gi_per_frame=gi, comm=comm)
+                r.sync()
+                best = min(best, (time.perf_counter() - t0) / frames * 1e6)
+            comm.close()
+            print(f"  tile {T:2d}, one rank holding every tile: local untile {local:7.1f} us/frame, "
+                  f"RCCL path {best:7.1f} us/frame (whole frame {full:.1f})", flush=True)
+        dist.destroy_process_group()
     if gi and os.environ.get("PROBE_STAGES"):
         # one frame at a time (no pipelining): stand-alone launch time of each stage for
         # rank 0's share -- which part's longest wave bounds a pipelined launch
