@@ -30,12 +30,13 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--fpl", type=int, default=8, help="frames per launch of the profiled bench run")
     ap.add_argument("--prefix", default="", help="pass directories pmc_<prefix>* only (gpu_run.sh PMC_TAG)")
+    ap.add_argument("--grid", type=int, default=0, help="dispatches of this Grid_Size only (e.g. the full-group launches)")
     a = ap.parse_args()
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(a.dir, f"pmc_{a.prefix}*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
-            if a.kernel not in name:
+            if a.kernel not in name or (a.grid and int(row.get("Grid_Size", 0)) != a.grid):
                 continue
             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
