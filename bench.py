@@ -148,6 +148,11 @@ def main():
     atlas = load_atlas()
 
     # ---------------------------------------------------------------- world
+    if world_size > 1:
+        # N > 1: the native loop's groups alternate over two streams, so one group's tail overlaps the
+        # next (one rank's C2 share at 8 ranks 19.6 -> 19.1 us/frame, profiles/r01_shard_probe_c2_streams.log);
+        # one GPU keeps one stream so each launch runs alone and its event time is the kernel's own
+        os.environ.setdefault("RV_BATCH_STREAMS", "2")
     r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=flags, atlas=atlas, device=local_rank)
     # the frame stream runs at the highest priority: the library's GI side
     # stream is created at the lowest, so the GI kernel fills the frame's gaps

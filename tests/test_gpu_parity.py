@@ -481,3 +481,29 @@ def test_pipelined_frames_stats(rv, atlas):
     assert three[0]["traces"] == 3 * one[0]["traces"]          # pre-pass: frame 0 + two pipelined
     assert three[7]["gi_traces"] > 0
     r.close()
+
+
+def test_render_frames_two_streams(rv, atlas, monkeypatch):
+    """RV_BATCH_STREAMS=2 (what bench.py uses with N > 1): groups alternate over
+    two streams so one group's tail overlaps the next; frames must not change --
+    whole frames, a one-rank shard and the one-rank RCCL gather path."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    monkeypatch.setenv("RV_BATCH_STREAMS", "2")
+    lg, W, H, T = 7, 320, 192, 16
+    ref = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=8, gi_sweeps=1)
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P1"], W, H)
+    ref.frame(cam, vp)
+    want = ref.readback(rv.RV_IMAGE_COLOR).copy()
+    r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=8, gi_sweeps=1)
+    r.set_frames_in_flight(4)
+    r.render_frames(11, cam, vp)
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), want)
+    r.set_tile_shard(T, 0, 1)
+    r.render_frames(9, cam, vp)
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), want)
+    comm = rv.Comm(r, rv.Comm.unique_id(), 1, 0)
+    r.render_frames(13, cam, vp, comm=comm)
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), want)
+    comm.close()
+    r.close()
+    ref.close()
