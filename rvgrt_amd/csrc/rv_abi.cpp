@@ -117,7 +117,7 @@ struct rv_ctx {
     int sched = SCHED_COST;
     int order_every = 4;          // RV_ORDER_EVERY: frames between chunk re-orderings
     int pipe = 1;                 // rv_set_pipeline / RV_PIPE: pipelined reference frames
-    uint32_t pipe_order = 0x012;  // RV_PIPE_ORDER: dispatch order of the parts, hex digits PIPE_* (first = high)
+    uint32_t pipe_order = 0x102;  // RV_PIPE_ORDER: dispatch order, hex digits PIPE_* (first = high): pre-pass, GI, render
     float* pipe_half[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [k & 1] {dist, shadow}
     bool gi_stats = false;        // rv_set_gi_stats
     // pipelined tile loop: packed tiles / rank-0 gather buffers per frame parity, GI shard staging
