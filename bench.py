@@ -3,17 +3,20 @@
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N>1
 launched by torch.distributed.run, one rank per GPU.  One step = one frame
-of the configured workload (default C2 = BASELINE.json configs[1]: 512^3
-procedural world, 1920x1080, primary + 1 sun-shadow ray per pixel), inputs
-resident in HBM.  W untimed frames, then K timed frames bracketed by a
-barrier + device synchronize on both sides; the time is the max over ranks.
-Rank 0 prints ONE JSON line.
+of the configured workload, inputs resident in HBM.  Default C4 (BASELINE
+configs[3], the north star's 1-GPU target): 1024^3 procedural world,
+3840x2160, the reference frame (half-res pre-pass, water reflection +
+reflection shadow, 6-cone voxel GI) over a GI grid after 2 full sweeps, with
+the reference's per-frame GI update (UpdateGIData, 262144 cells) before every
+frame.  W untimed frames, then K timed frames bracketed by a barrier +
+device synchronize on both sides; the time is the max over ranks.  Rank 0
+prints ONE JSON line.
 
-Multi-GPU: the frame is split into interleaved 64x64 screen tiles (round
-robin over ranks), every rank renders its tiles of the same frame against
-its own locally generated replica of the world, and rank 0 gathers the
-packed RGBA8 tiles over RCCL (torch.distributed "nccl") and scatters them
-into the frame: strong scaling of a fixed frame.
+Multi-GPU: the frame is split into interleaved screen tiles (rv_set_tile_shard),
+every rank renders its tiles of the same frame against its own locally
+generated replica of the world and 1/N of the GI update's cells (RCCL
+all-gather), and rank 0 gathers the packed tiles over RCCL and assembles the
+frame: strong scaling of a fixed frame.
 """
 from __future__ import annotations
 
@@ -75,7 +78,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", help="c1..c5 (default c2 = BASELINE configs[1])")
+    ap.add_argument("--config", default="c4",
+                    help="c1..c5 (default c4: 1024^3, 3840x2160, the reference frame with 2-bounce GI and a GI "
+                         "update every frame -- the north star's 1-GPU workload, BASELINE configs[3])")
     ap.add_argument("--pose", default="P0")
     ap.add_argument("--tile-px", type=int, default=None,
                     help="screen-tile size of the N>1 shard (default: 16 px without the pre-pass, 32 with it; "
@@ -85,7 +90,7 @@ def main():
                     help="N>1 native loop: rank 0's share of tiles relative to the others (rank 0 also receives "
                          "and assembles every frame); default 1 - 0.019 (N-1): its measured assembly cost is "
                          "1.9%% of a whole frame's render (profiles/r01_shard_probe_c2_root.log)")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0,
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
     ap.add_argument("--path", default="fused", choices=["fused", "wavefront"],
@@ -373,6 +378,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # single-frame latency: one frame per call, submitted and waited for alone (median of 9)
+    lat = []
+    if native:
+        for _ in range(9):
+            barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            run_native(1)
+            torch.cuda.synchronize(dev)
+            lat.append((time.perf_counter() - t1) * 1000.0)
+    latency_ms = round(float(np.median(lat)), 4) if lat else None
+
     gather_check = None
     if world_size > 1 and rank == 0:   # the gathered frame must equal a one-GPU frame
         tiled = r.readback(rv.RV_IMAGE_COLOR).copy()
@@ -451,6 +468,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(fps, 2),
+            "latency_ms": latency_ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -487,10 +505,14 @@ def main():
 
 
 def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
-    """The CPU oracle (scalar DDA restatement) on the host cores, same world
-    (exported from the GPU; bit-identical to the oracle's own build, see
-    tests/test_gpu_parity.py), same camera and features.  Bounded sample:
-    whole frames until the budget is spent, else a stride-k row subset."""
+    """The CPU oracle (scalar DDA restatement, oracle/rv_oracle.c) on the host
+    cores: same world (exported from the GPU; bit-identical to the oracle's
+    own build, tests/test_gpu_parity.py), same camera and features, the frame
+    render only (as rays_per_frame counts it).  Bounded sample:
+    frames of <= 1080p are rendered whole, row band by row band in a spread
+    order, until the budget is spent; 4K frames take the stride-16 row subset
+    (rows y = 0 mod 16, i.e. 1/16 of the frame) in spread chunks.  The rate is
+    traces / wall time, so a partial sample extrapolates by ray count."""
     import rvgrt_amd as rv
     from oracle import oracle as O
 
@@ -501,38 +523,36 @@ def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
     w.csdf[:] = r.world_export(rv.RV_WORLD_CSDF)
     w.gi[:] = r.world_export(rv.RV_WORLD_GI)
     fr = O.make_frame(cfg.width, cfg.height, flags, rv.camera_dict(cam, vp))
-    # bands of rows spread over the image (OpenMP parallel over a band's rows)
     H = cfg.height
-    band = max(8, 2 * threads)
-    starts = list(range(0, H, band))
-    order = [s for k in range(4) for s in starts[k::4]]
-    t0 = time.perf_counter()
-    rays = rows = 0
-    done = False
-    while not done:            # whole frames (row bands in a spread order) until the budget is spent
-        for s in order:
-            out = O.render(w, fr, s, min(H, s + band))
-            rays += out["stats"]["traces"]
-            rows += min(H, s + band) - s
-            if time.perf_counter() - t0 >= budget_s:
-                done = True
-                break
-    dt = time.perf_counter() - t0
-    # the 1-core figure: the same bands on one thread, ~1/4 of the budget
-    O.set_threads(1)
-    t1 = time.perf_counter()
-    rays1 = 0
-    for s in order:
-        rays1 += O.render(w, fr, s, min(H, s + band))["stats"]["traces"]
-        if time.perf_counter() - t1 >= budget_s / 4:
-            break
-    dt1 = time.perf_counter() - t1
+    stride = 16 if cfg.width * cfg.height > 1920 * 1080 else 1
+    rows_all = np.arange(0, H, stride, dtype=np.int32)
+    chunk = max(4 * threads, 32)
+    chunks = [rows_all[i:i + chunk] for i in range(0, len(rows_all), chunk)]
+    order = [c for k in range(4) for c in chunks[k::4]]        # spread over the image
+    out = None
+
+    def run(budget):
+        nonlocal out
+        t0 = time.perf_counter()
+        rays = rows = 0
+        while True:
+            for c in order:
+                out = O.render_rows(w, fr, c, out=out)
+                rays += out["stats"]["traces"]
+                rows += len(c)
+                if time.perf_counter() - t0 >= budget:
+                    return rays, rows, time.perf_counter() - t0
+
+    rays, rows, dt = run(budget_s)
+    O.set_threads(1)                           # the 1-core figure, ~1/4 of the budget
+    rays1, _, dt1 = run(budget_s / 4)
     O.set_threads(threads)
+    what = (f"stride-{stride} row subset ({len(rows_all)} of {H} rows)" if stride > 1 else "whole frames")
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "value_1core": round(rays1 / dt1 / 1e6, 3),
-            "sample": f"oracle/rv_oracle.c render of {rows} rows ({rows / H:.2f} frames) of {cfg.name} in "
-                      f"{band}-row bands on {threads} threads ({dt:.1f}s wall, {rays} traces), "
-                      "same world/camera/flags"}
+            "sample": f"oracle/rv_oracle.c render of {what} of {cfg.name}: {rows} rows ({rows / H:.2f} frame "
+                      f"heights) in {chunk}-row chunks on {threads} threads, {dt:.1f} s wall, {rays} traces, "
+                      "same world/camera/flags; Mrays/s = traces / wall time"}
 
 
 if __name__ == "__main__":

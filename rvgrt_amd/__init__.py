@@ -5,7 +5,7 @@ and the raytracing_functions it calls), rebuilt as hand-written HIP kernels
 for gfx950 behind the C ABI in include/rvgrt.h (librvgrt_hip.so).
 """
 from . import _lib
-from ._lib import (RV_F_GI, RV_F_PREPASS, RV_F_SHADOW, RV_F_STATS, RV_F_WATER,
+from ._lib import (RV_F_GI, RV_F_PREPASS, RV_F_REF_FETCH, RV_F_SHADOW, RV_F_STATS, RV_F_WATER,
                    RV_FLAGS_REFERENCE, RV_IMAGE_COLOR, RV_IMAGE_DEPTH, RV_IMAGE_HALF_DIST,
                    RV_IMAGE_HALF_SHADOW, RV_IMAGE_MOTION, RV_WORLD_BITS, RV_WORLD_CSDF,
                    RV_WORLD_GI, RvError)
@@ -13,7 +13,7 @@ from .configs import CONFIGS, RenderConfig
 from .render import Comm, StateRender, camera_dict, camera_from_pose
 
 __all__ = ["StateRender", "Comm", "camera_from_pose", "camera_dict", "CONFIGS", "RenderConfig", "RvError",
-           "RV_F_GI", "RV_F_PREPASS", "RV_F_SHADOW", "RV_F_STATS", "RV_F_WATER",
+           "RV_F_GI", "RV_F_PREPASS", "RV_F_REF_FETCH", "RV_F_SHADOW", "RV_F_STATS", "RV_F_WATER",
            "RV_FLAGS_REFERENCE", "RV_IMAGE_COLOR", "RV_IMAGE_DEPTH", "RV_IMAGE_HALF_DIST",
            "RV_IMAGE_HALF_SHADOW", "RV_IMAGE_MOTION", "RV_WORLD_BITS", "RV_WORLD_CSDF",
            "RV_WORLD_GI", "_lib"]

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RVGRT_LIB") or os.path.join(_HERE, "librvgrt_hip.so")
 
 RV_OK, RV_ERR_INVALID, RV_ERR_HIP, RV_ERR_OOM, RV_ERR_STATE, RV_ERR_NO_DEVICE = range(6)
-RV_F_PREPASS, RV_F_WATER, RV_F_GI, RV_F_SHADOW, RV_F_STATS = 1, 2, 4, 8, 16
+RV_F_PREPASS, RV_F_WATER, RV_F_GI, RV_F_SHADOW, RV_F_STATS, RV_F_REF_FETCH = 1, 2, 4, 8, 16, 32
 RV_FLAGS_REFERENCE = RV_F_PREPASS | RV_F_WATER | RV_F_GI
 RV_IMAGE_COLOR, RV_IMAGE_MOTION, RV_IMAGE_DEPTH, RV_IMAGE_HALF_DIST, RV_IMAGE_HALF_SHADOW = range(5)
 RV_WORLD_BITS, RV_WORLD_CSDF, RV_WORLD_GI = range(3)

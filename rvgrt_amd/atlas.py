@@ -8,6 +8,7 @@ for the offscreen framebuffer dump that replaces the D3D12 present path.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import struct
 import zlib
@@ -88,11 +89,17 @@ _ATLAS_CACHE = None
 
 
 def load_atlas() -> np.ndarray:
-    """The reference texture atlas as a (256, 256, 4) uint8 array (row 0 = top)."""
+    """The reference texture atlas as a (256, 256, 4) uint8 array (row 0 = top).
+    The asset must be the reference's resources/texturepack.png byte for byte
+    (ATLAS_SHA256); a different file raises instead of rendering other pixels."""
     global _ATLAS_CACHE
     if _ATLAS_CACHE is None:
         with open(ATLAS_PNG, "rb") as f:
-            _ATLAS_CACHE = decode_png(f.read())
+            data = f.read()
+        digest = hashlib.sha256(data).hexdigest()
+        if digest != ATLAS_SHA256:
+            raise ValueError(f"{ATLAS_PNG}: sha256 {digest} is not the reference atlas {ATLAS_SHA256}")
+        _ATLAS_CACHE = decode_png(data)
     return _ATLAS_CACHE
 
 

@@ -893,6 +893,7 @@ rv_status rv_draw_cuda(rv_ctx* c, const float pos[3], const float fo[3], const f
         // c_time = c_cam[17] = host jitterY; c_jitterX = c_cam[18] (never
         // written, 0); c_jitterY = c_cam[19] (4 B past the symbol).
         time = jitter_y; jx = 0.0f; jy = c->cfg.ref_oob_jy;
+        return rv_frame(c, &cam, vp16, pvp16, time, jx, jy, c->cfg.flags | RV_F_REF_FETCH);
     } else {
         long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(
                            std::chrono::system_clock::now().time_since_epoch()).count();
@@ -1825,14 +1826,9 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
     int prio = 0;   // slot streams run at the caller stream's priority
     if (c->stream) HIP_TRY(c, hipStreamGetPriority(c->stream, &prio));
     if (!c->fstreams.empty() && c->fstream_prio != prio) {
+        // only the streams depend on the priority; batch buffers and events stay
         HIP_TRY(c, hipDeviceSynchronize());
-        for (BatchSet& b : c->bsets) {
-        hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
-        hipFree(b.tbuf); hipFree(b.gbuf);
-        if (b.rendered) hipEventDestroy(b.rendered);
-        if (b.gathered) hipEventDestroy(b.gathered);
-    }
-    for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
+        for (hipStream_t fs : c->fstreams) hipStreamDestroy(fs);
         c->fstreams.clear();
     }
     c->fstream_prio = prio;

@@ -125,13 +125,68 @@ RV_HD uint32_t csdf_off(const World& w, uint32_t cx, uint32_t cy, uint32_t cz) {
     return (brick_byte(w, cx >> 2, cy >> 2, cz >> 2) + w.coff) | ((cy & 3u) << 2) | ((cz & 3u) << 4);
 }
 RV_HD uint32_t csdf_byte(uint32_t word, uint32_t cx) { return (word >> ((cx & 3u) << 3)) & 255u; }
-RV_HD uint32_t csdf_at(const World& w, int cx, int cy, int cz) {
-    return csdf_byte(load_dword(w, csdf_off(w, (uint32_t)cx, (uint32_t)cy, (uint32_t)cz)), (uint32_t)cx);
+
+// Layout accessors the traversal is written against (trace<..., WV>): a
+// dword locator and its load for the CSDF and for the voxel bits, and the bit
+// of voxel (x, y) inside its word.  World = the brick layout above;
+// LinearWorld (below) = the reference's own layout.
+RV_HD uint32_t csdf_load(const World& w, uint32_t off) { return load_dword(w, off); }
+RV_HD uint32_t voxel_load(const World& w, uint32_t off) { return load_dword(w, off); }
+RV_HD uint32_t voxel_bit(const World&, uint32_t x, uint32_t y) { return voxel_bit(x, y); }
+RV_HD uint32_t gi_texel(const World& w, uint64_t idx) { return w.gi[idx]; }
+
+// The reference's layouts (include/cumath.cuh:33-45, include/CoarseArray.cuh:
+// 9-21): bit idx = x | y<<lx | z<<(lx+ly) in uint32 words, CSDF bytes x
+// fastest, GI RGBA8 x fastest.  Used by the reference-signature device API
+// (include/rvgrt_device.h), not by the frame kernels.  Needs X >= 32 (the
+// word's 32 bits are x-consecutive) and < 2^34 voxels (32-bit offsets).
+struct LinearWorld {
+    const uint32_t* __restrict__ bits;
+    const uint8_t* __restrict__ csdf;
+    const uint32_t* __restrict__ gi;
+    const uint32_t* __restrict__ atlas;
+    int X, Y, Z;
+    int lx, lxy;                         // log2 X, log2 (X*Y)
+    int SX, SY, SZ;
+    int GX, GY, GZ;
+    int aw, ah;
+};
+RV_HD LinearWorld linear_world(int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf,
+                               const uint32_t* gi = nullptr, const uint32_t* atlas = nullptr, int aw = 256,
+                               int ah = 256) {
+    LinearWorld w;
+    w.bits = bits; w.csdf = csdf; w.gi = gi; w.atlas = atlas;
+    w.X = 1 << lx; w.Y = 1 << ly; w.Z = 1 << lz;
+    w.lx = lx; w.lxy = lx + ly;
+    w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
+    w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
+    w.aw = aw; w.ah = ah;
+    return w;
+}
+RV_HD uint32_t csdf_off(const LinearWorld& w, uint32_t cx, uint32_t cy, uint32_t cz) {
+    return (cx | (cy << (w.lx - 1)) | (cz << (w.lxy - 2))) & ~3u;   // dword holding byte cz*SX*SY + cy*SX + cx
+}
+RV_HD uint32_t csdf_load(const LinearWorld& w, uint32_t off) {
+    return *reinterpret_cast<const uint32_t*>(w.csdf + off);
+}
+RV_HD uint32_t voxel_word_off(const LinearWorld& w, uint32_t x, uint32_t y, uint32_t z) {
+    return ((x >> 5) | (y << (w.lx - 5)) | (z << (w.lxy - 5))) << 2;
+}
+RV_HD uint32_t voxel_load(const LinearWorld& w, uint32_t off) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.bits) + off);
+}
+RV_HD uint32_t voxel_bit(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
+RV_HD uint32_t gi_texel(const LinearWorld& w, uint64_t idx) { return w.gi[idx]; }
+
+template <class WV>
+RV_HD uint32_t csdf_at(const WV& w, int cx, int cy, int cz) {
+    return csdf_byte(csdf_load(w, csdf_off(w, (uint32_t)cx, (uint32_t)cy, (uint32_t)cz)), (uint32_t)cx);
 }
 
 // getDistance(float3) (include/raytracing_functions.cuh:35-51): truncating
 // cast after floorf*0.5, clamped to the grid (Appendix R11).
-RV_HD float get_distance_f(const World& w, f3 p) {
+template <class WV>
+RV_HD float get_distance_f(const WV& w, f3 p) {
     int cx = (int)(floorf(p.x) * 0.5f);
     int cy = (int)(floorf(p.y) * 0.5f);
     int cz = (int)(floorf(p.z) * 0.5f);
@@ -142,7 +197,8 @@ RV_HD float get_distance_f(const World& w, f3 p) {
 }
 
 // getDistance(int3) (include/raytracing_functions.cuh:52-67).
-RV_HD uint32_t get_distance_i(const World& w, int x, int y, int z) {
+template <class WV>
+RV_HD uint32_t get_distance_i(const WV& w, int x, int y, int z) {
     int cx = x / 2, cy = y / 2, cz = z / 2;
     cx = imax(imin(cx, w.SX - 1), 0);
     cy = imax(imin(cy, w.SY - 1), 0);
@@ -283,6 +339,7 @@ struct Hit {
 
 struct StepCount {  // per-trace work counters (algorithmic bytes)
     uint32_t sphere, dda, check;
+    uint32_t its;   // hitInfo.its: major iterations + DDA loop entries (raytracing_functions.cu:107,124)
 };
 
 // trace (src/raytracing_functions.cu:85-202) with approximateCSDF (:65-83)
@@ -307,8 +364,8 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 #define RV_WORD_REUSE 0
 #endif
 
-template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0)>
-RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
+template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0), class WV = World>
+RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
     H.hit = false; H.undef = false; H.its = 0;
     H.pos = V(-500.0f, -500.0f, -500.0f);
@@ -327,6 +384,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     int status = 0;   // 0: gave up (miss), 2: left the grid (miss), 3: hit
     uint32_t c_off = 0xFFFFFFFFu, c_word = 0, v_off = 0xFFFFFFFFu, v_word = 0;   // REUSE: last gathers
     for (int major = 0; major < 5; major++) {
+        if (COUNT) sc.its++;
         // ---- approximateCSDF: sphere-step through the coarse SDF.  The body
         // is straight-line (clamped, always-valid gather; predicated update)
         // with a single exit, so a wave pays no divergent-branch bookkeeping.
@@ -340,7 +398,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             uint32_t d;
             if (REUSE) {   // gather only where the CSDF dword changed
                 const uint32_t off = csdf_off(w, cx, cy, cz);
-                if (off != c_off) { c_word = load_dword(w, off); c_off = off; }
+                if (off != c_off) { c_word = csdf_load(w, off); c_off = off; }
                 d = csdf_byte(c_word, cx);
             } else {
                 d = csdf_at(w, (int)cx, (int)cy, (int)cz);
@@ -353,7 +411,11 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             cur.z = stop ? cur.z : nxt.z;
             if (stop) break;
         }
-        if (oob) { status = 2; break; }
+        if (oob) {            // the reference's DDA then fails its bounds test at i = 0
+            if (COUNT) sc.its++;
+            status = 2;
+            break;
+        }
         // ---- DDA set-up
         ix = (int)floorf(cur.x); iy = (int)floorf(cur.y); iz = (int)floorf(cur.z);
         tx = ((sx > 0) ? ((float)ix + 1.0f - cur.x) : (cur.x - (float)ix)) * ddx;
@@ -384,10 +446,10 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                         uint32_t cx = (uint32_t)imin(imax(jx >> 1, 0), w.SX - 1);
                         uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
                         uint32_t cz = (uint32_t)imin(imax(jz >> 1, 0), w.SZ - 1);
-                        cw = load_dword(w, csdf_off(w, cx, cy, cz));
+                        cw = csdf_load(w, csdf_off(w, cx, cy, cz));
                     }
                     const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
-                    wv[j] = load_dword(w, voxel_word_off(w, qx, qy, qz));
+                    wv[j] = voxel_load(w, voxel_word_off(w, qx, qy, qz));
                     const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
                     const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
                     ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
@@ -396,6 +458,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             }
 #pragma unroll
             for (int j = 0; j < G; j++) {
+                if (COUNT) sc.its++;
                 if (j == G - 1 && chk) {
                     uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
                     jd = csdf_byte(cw, cx);
@@ -403,7 +466,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                     st = jd > 2 ? 1 : 0;
                 }
                 const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
-                const bool solid = (wv[j] >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
+                const bool solid = (wv[j] >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
                 if (COUNT) sc.dda += (st == 0) & !oob;
                 st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
                 const bool go = st == 0;
@@ -423,6 +486,7 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         }
         } else {
         for (int i = 0; i < 200; i++) {
+            if (COUNT) sc.its++;
             if ((i & 7) == 7) {   // i is wave-uniform: a scalar branch
                 uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
                 uint32_t cy = (uint32_t)imin(imax(iy >> 1, 0), w.SY - 1);
@@ -437,12 +501,12 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             uint32_t word;
             if (REUSE) {   // a word covers 8 (x) x 4 (y) voxels: runs along x/y re-read it
                 const uint32_t off = voxel_word_off(w, qx, qy, qz);
-                if (off != v_off) { v_word = load_dword(w, off); v_off = off; }
+                if (off != v_off) { v_word = voxel_load(w, off); v_off = off; }
                 word = v_word;
             } else {
-                word = load_dword(w, voxel_word_off(w, qx, qy, qz));
+                word = voxel_load(w, voxel_word_off(w, qx, qy, qz));
             }
-            const bool solid = (word >> voxel_bit((uint32_t)ix, (uint32_t)iy)) & 1u;
+            const bool solid = (word >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
             if (COUNT) sc.dda += (st == 0) & !oob;
             st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
             const bool go = st == 0;
@@ -500,8 +564,8 @@ RV_HD Hit trace(const World& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
 #define RV_TAN_CONE 0.42279321873816174f
 
 // traceCone (src/raytracing_functions.cu:212-273)
-template <bool COUNT>
-RV_HD f3 trace_cone(const World& w, f3 pos, f3 dir, uint32_t& steps) {
+template <bool COUNT, class WV = World>
+RV_HD f3 trace_cone(const WV& w, f3 pos, f3 dir, uint32_t& steps) {
     f3 acc = V(0.0f, 0.0f, 0.0f);
     float alpha = 0.0f;
     float cd = 1.5f * 2.0f;
@@ -516,7 +580,7 @@ RV_HD f3 trace_cone(const World& w, f3 pos, f3 dir, uint32_t& steps) {
         int gy = (int)(floorf(p.y) / 4.0f);
         int gz = (int)(floorf(p.z) / 4.0f);
         if (gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ) {
-            uint32_t s = w.gi[(uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx];
+            uint32_t s = gi_texel(w, (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx);
             f3 c = V((float)(s & 255u) / 255.0f, (float)((s >> 8) & 255u) / 255.0f,
                      (float)((s >> 16) & 255u) / 255.0f);
             float a = (float)(s >> 24) / 255.0f;
@@ -539,7 +603,8 @@ RV_HD f3 sample_sky(f3 dir, f3 sun) {
 // sampleTexture (src/raytracing_functions.cu:28-62): fp16 UV math, the
 // +121.3 offsets added in double (:43), swapped atlas coords (R10),
 // point filter + wrap on a 256x256 RGBA8 atlas, texel = byte/255.
-RV_HD f3 sample_texture(const World& w, float u, float v, f3 pos) {
+template <class WV>
+RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
     const float freq = 0.05f;
     float e = simplex3D(floorf(pos.x) * freq, floorf(pos.y) * freq, floorf(pos.z) * freq);
     float e2 = simplex3D(floorf((float)((double)pos.x + 121.3)) * freq * 0.3f,

@@ -122,11 +122,27 @@ __device__ __forceinline__ void chunk_cost_report(uint32_t* cost, uint64_t t0, u
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// minDist (StateRender.cu:182-198) with W/2 x H/2 (Appendix R6)
+// minDist (StateRender.cu:182-198) with W/2 x H/2 (Appendix R6).  The
+// reference fetches with normalized coordinates: u_low = floor(x*640)/640 and
+// u_low + 1/640, each turned back into a texel by the point-sampling unit as
+// floor(u*640); RV_F_REF_FETCH restates that float path (the quad can land a
+// texel low where k/640*640 rounds below k), otherwise the texels are the
+// exact k, k+1.
 __device__ __forceinline__ float min_dist(const FrameParams& f, float x, float y) {
-    int u = (int)floorf(x * (float)f.hw), v = (int)floorf(y * (float)f.hh);
-    int u1 = clampi(u + 1, 0, f.hw - 1), v1 = clampi(v + 1, 0, f.hh - 1);
-    u = clampi(u, 0, f.hw - 1); v = clampi(v, 0, f.hh - 1);
+    int u, v, u1, v1;
+    if (f.flags & RV_F_REF_FETCH) {   // wave-uniform: a scalar branch
+        const float fw = (float)f.hw, fh = (float)f.hh;
+        const float ul = floorf(x * fw) / fw, vl = floorf(y * fh) / fh;
+        const float px = 1.0f / fw, py = 1.0f / fh;
+        u = clampi((int)floorf(ul * fw), 0, f.hw - 1);
+        u1 = clampi((int)floorf((ul + px) * fw), 0, f.hw - 1);
+        v = clampi((int)floorf(vl * fh), 0, f.hh - 1);
+        v1 = clampi((int)floorf((vl + py) * fh), 0, f.hh - 1);
+    } else {
+        u = (int)floorf(x * (float)f.hw); v = (int)floorf(y * (float)f.hh);
+        u1 = clampi(u + 1, 0, f.hw - 1); v1 = clampi(v + 1, 0, f.hh - 1);
+        u = clampi(u, 0, f.hw - 1); v = clampi(v, 0, f.hh - 1);
+    }
     const float* hd = f.hdist;
     float d1 = hd[(size_t)v * f.hw + u], d2 = hd[(size_t)v * f.hw + u1];
     float d3 = hd[(size_t)v1 * f.hw + u], d4 = hd[(size_t)v1 * f.hw + u1];

@@ -59,3 +59,42 @@ def random_rays(rng, n, dims, inside_frac=0.7):
     dist = rng.uniform(-10, 40, n).astype(np.float32)
     dist[rng.uniform(size=n) < 0.3] = 0.0
     return org, d.astype(np.float32), dist
+
+
+class Hip:
+    """Streams and device buffers from the HIP runtime the library loaded
+    (the test must not bring in a second runtime through torch)."""
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.L = C.CDLL("libamdhip64.so.7")
+        self.owned = []
+
+    def stream(self, priority=None):
+        s = self.C.c_void_p()
+        if priority is None:
+            assert self.L.hipStreamCreate(self.C.byref(s)) == 0
+        else:
+            assert self.L.hipStreamCreateWithPriority(self.C.byref(s), 0, int(priority)) == 0
+        self.owned.append(("s", s))
+        return s.value
+
+    def download2d(self, ptr, pitch, row_bytes, rows):
+        """Copy a pitched device image to a host (rows, pitch) uint8 array."""
+        import numpy as np
+        out = np.zeros((rows, pitch), np.uint8)
+        assert self.L.hipMemcpy(out.ctypes.data_as(self.C.c_void_p), self.C.c_void_p(ptr),
+                                self.C.c_size_t(rows * pitch), 2) == 0   # hipMemcpyDeviceToHost
+        return out
+
+    def malloc(self, n):
+        p = self.C.c_void_p()
+        assert self.L.hipMalloc(self.C.byref(p), self.C.c_size_t(n)) == 0
+        assert self.L.hipMemset(p, 0, self.C.c_size_t(n)) == 0
+        self.owned.append(("m", p))
+        return p.value
+
+    def close(self):
+        self.L.hipDeviceSynchronize()
+        for kind, h in self.owned:
+            (self.L.hipStreamDestroy if kind == "s" else self.L.hipFree)(h)

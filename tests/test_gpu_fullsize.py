@@ -1,7 +1,13 @@
-"""GPU parity at BASELINE.json's full sizes (C2 512^3, C3/C4
-1024^3, C5 2048^3), where rebuilding the whole world on the CPU oracle is too
-slow for a test.  The GPU world is exported and checked with properties and
-samples the oracle can answer at any size:
+"""GPU parity at BASELINE.json's full sizes and at the reference's own native
+configuration (C1 256^3 @ 640x360, C2 512^3 @ 1080p, C3 1024^3 @
+1080p, C4 1024^3 @ 2160p with 2 GI sweeps, C5 2048^3 @ 2160p; the reference's
+4096 x 512 x 4096 world at 1280 x 800 through drawCUDA with ref_compat,
+include/cumath.cuh:19-31, include/State.hpp:28-29).
+
+C1 is small enough for the oracle to build the whole world and render the
+whole frame.  Above it, where an oracle world build is too slow for a test,
+the GPU world is exported and checked with what the oracle answers at any
+size:
 
 * voxel bits: 200k sampled voxels against the oracle's Evaluate (> 0.7);
 * CSDF: zero exactly where a coarse 2x2x2 cell holds a solid voxel, over the
@@ -9,8 +15,8 @@ samples the oracle can answer at any size:
 * traversal: 20k random rays traced on the GPU and by the oracle on the
   exported world, bit-exact (32-bit brick offsets up to 2 GiB of records);
 * GI: a RAYPS-style partial update window, GPU vs oracle on the same grid;
-* frames: sampled rows of the config's frame (its resolution and flags),
-  GPU vs oracle render of the same rows on the exported world.
+* frames: sampled rows of the config's frame (its resolution, flags and
+  pose), GPU vs oracle render of the same rows on the exported world.
 """
 import ctypes as C
 
@@ -29,44 +35,48 @@ def rv():
     return rvgrt_amd
 
 
-@pytest.mark.parametrize("cfgname", ["c2", "c3", "c5"])
-def test_fullsize_world_traversal_gi_frame_rows(rv, atlas, oracle, cfgname):
-    from rvgrt_amd.configs import CONFIGS, pose_f32
-    cfg = CONFIGS[cfgname]
-    lg, n = cfg.log2_n, cfg.n
-    W, H = cfg.width, cfg.height
-    r = rv.StateRender((lg,) * 3, W, H, flags=cfg.flags, atlas=atlas)
-    r.world_build()
-    for s in range(max(cfg.gi_sweeps, 0)):
-        r.gi_update(s)
-    r.sync()
-    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas)
+def coarse_solid(bits, dims, z0, z1):
+    """Coarse 2x2x2 cells of voxel slices [z0, z1) holding a solid voxel, from
+    the canonical bit words (x fastest, little bit order), as bool (z, y, x)."""
+    X, Y, Z = dims
+    v = bits.view(np.uint8).reshape(Z, Y, X // 8)[z0:z1]
+    v = np.bitwise_or.reduce(v.reshape(-1, 2, Y, X // 8), axis=1)
+    v = np.bitwise_or.reduce(v.reshape(v.shape[0], Y // 2, 2, X // 8), axis=2)
+    v = v | (v >> 1)                                       # x pairs inside a byte -> even bits
+    b = np.unpackbits(v, axis=-1, bitorder="little").reshape(v.shape[0], Y // 2, X // 8, 8)[..., ::2]
+    return b.reshape(v.shape[0], Y // 2, X // 2).astype(bool)
+
+
+def check_world_rays_gi(r, rv, oracle, atlas, log2, seed, gi_window=True):
+    """The exported GPU world against the oracle's answers; returns the oracle
+    world holding it."""
+    lx, ly, lz = log2
+    X, Y, Z = 1 << lx, 1 << ly, 1 << lz
+    ow = oracle.OracleWorld(lx, ly, lz, atlas=atlas)
     ow.bits[:] = r.world_export(rv.RV_WORLD_BITS)
     ow.csdf[:] = r.world_export(rv.RV_WORLD_CSDF)
     ow.gi[:] = r.world_export(rv.RV_WORLD_GI)
-    rng = np.random.default_rng(lg)
+    rng = np.random.default_rng(seed)
 
     # voxel bits vs Evaluate at sampled voxels
     m = 200_000
-    xyz = rng.integers(0, n, size=(m, 3))
+    xyz = rng.integers(0, [X, Y, Z], size=(m, 3))
     p = np.ascontiguousarray(xyz.astype(np.float32))
     val = np.zeros(m, np.float32)
     oracle.lib().or_evaluate_batch(p.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p), m)
-    idx = xyz[:, 0].astype(np.int64) | (xyz[:, 1].astype(np.int64) << lg) | (xyz[:, 2].astype(np.int64) << (2 * lg))
+    idx = xyz[:, 0].astype(np.int64) | (xyz[:, 1].astype(np.int64) << lx) | (xyz[:, 2].astype(np.int64) << (lx + ly))
     got = (ow.bits[idx >> 5] >> (idx & 31).astype(np.uint32)) & 1
     assert np.array_equal(got.astype(bool), val > 0.7)
 
-    # CSDF zero <=> coarse cell solid, whole grid (done in z slabs to bound memory)
-    cs = ow.csdf.reshape(n // 2, n // 2, n // 2)
-    v = ow.bits.view(np.uint8)
+    # CSDF zero <=> coarse cell solid, whole grid, in z slabs
+    cs = ow.csdf.reshape(Z // 2, Y // 2, X // 2)
     slab = 64
-    for z0 in range(0, n, slab):
-        b = np.unpackbits(v[(z0 * n * n) // 8:((z0 + slab) * n * n) // 8], bitorder="little")
-        solid = b.reshape(slab // 2, 2, n // 2, 2, n // 2, 2).any(axis=(1, 3, 5))
-        assert np.array_equal(cs[z0 // 2:(z0 + slab) // 2] == 0, solid), f"z slab {z0}"
+    for z0 in range(0, Z, slab):
+        assert np.array_equal(cs[z0 // 2:(z0 + slab) // 2] == 0, coarse_solid(ow.bits, (X, Y, Z), z0, z0 + slab)), \
+            f"z slab {z0}"
 
     # traversal bit-exact on the exported world
-    org, dirs, dist = random_rays(rng, 20_000, (n, n, n))
+    org, dirs, dist = random_rays(rng, 20_000, (X, Y, Z))
     g = r.trace_rays(org, dirs, dist)
     o = ow.trace_batch(org, dirs, dist)
     assert np.array_equal(g["hit"], o["hit"]) and np.array_equal(g["undef"], o["undef"])
@@ -76,26 +86,103 @@ def test_fullsize_world_traversal_gi_frame_rows(rv, atlas, oracle, cfgname):
     assert np.array_equal(g["sphere_steps"], o["n_sphere"]) and np.array_equal(g["dda_steps"], o["n_dda"])
 
     # GI: one RAYPS window at a rolling offset, same grid on both sides
-    if cfg.gi_sweeps >= 0:
-        ncell = (n // 4) ** 3
+    if gi_window:
+        ncell = (X // 4) * (Y // 4) * (Z // 4)
         first, count = ncell // 3, 4096
         r.gi_update(7, first=first, count=count)
         ow.gi_update(7, first=first, count=count)
         assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi)
+    return ow
 
-    # sampled rows of the config's frame
-    pos, yaw, pitch = pose_f32(cfg)
-    cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
-    r.frame(cam, vp)
+
+def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=6):
     img = r.readback(rv.RV_IMAGE_COLOR)
     mv = r.readback(rv.RV_IMAGE_MOTION)
     dep = r.readback(rv.RV_IMAGE_DEPTH)
-    fr = oracle.make_frame(W, H, cfg.flags, rv.camera_dict(cam, vp))
-    rows = sorted(set(rng.integers(0, H, 6).tolist()) | {0, H // 2, H - 1})
+    fr = oracle.make_frame(W, H, flags, cam_d, time=time)
+    rows = sorted(set(rng.integers(0, H, nrows).tolist()) | {0, H // 2, H - 1})
     for y in rows:
         ref = oracle.render(ow, fr, y, y + 1, want_stats=False)
-        assert np.array_equal(img[y], ref["rgba"][y]), f"{cfgname} row {y}"
-        assert np.array_equal(mv[y], ref["mv"][y]) and np.array_equal(dep[y], ref["depth"][y])
+        assert np.array_equal(img[y], ref["rgba"][y]), f"row {y}"
+        assert np.array_equal(mv[y], ref["mv"][y]) and np.array_equal(dep[y], ref["depth"][y]), f"row {y}"
+    return rows
+
+
+def test_c1_full_world_full_frame(rv, atlas, oracle):
+    """C1 (BASELINE configs[0]: 256^3, 640x360, primary rays only) at its
+    size: the oracle builds the whole world and renders the whole frame."""
+    from rvgrt_amd.configs import CONFIGS, pose_f32
+    cfg = CONFIGS["c1"]
+    lg, W, H = cfg.log2_n, cfg.width, cfg.height
+    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas).build(gi_sweeps=0)
+    r = rv.StateRender((lg,) * 3, W, H, flags=cfg.flags, atlas=atlas)
+    r.world_build()
+    assert np.array_equal(r.world_export(rv.RV_WORLD_BITS), ow.bits)
+    assert np.array_equal(r.world_export(rv.RV_WORLD_CSDF), ow.csdf)
+    assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi)
+    for pose in ("P0", "P1"):
+        cam, vp = rv.camera_from_pose(*pose_f32(cfg, pose), W, H)
+        r.stats_reset()
+        r.frame(cam, vp, flags=cfg.flags | rv.RV_F_STATS)
+        img = r.readback(rv.RV_IMAGE_COLOR)
+        ref = oracle.render(ow, oracle.make_frame(W, H, cfg.flags, rv.camera_dict(cam, vp)))
+        d = np.abs(img.astype(np.int32) - ref["rgba"].astype(np.int32)).max(axis=2)
+        assert d.max() <= 2 and (d == 0).mean() >= 0.995, pose
+        assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"])
+        assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"])
+        st = r.stats()
+        for k in ("traces", "primary", "sphere_steps", "dda_steps", "csdf_checks", "tex_samples", "undef_hits"):
+            assert st[k] == ref["stats"][k], (pose, k)
+    r.close()
+
+
+@pytest.mark.parametrize("cfgname,pose", [("c2", "P0"), ("c3", "P0"), ("c3", "P1"), ("c4", "P0"), ("c5", "P0")])
+def test_fullsize_world_traversal_gi_frame_rows(rv, atlas, oracle, cfgname, pose):
+    from rvgrt_amd.configs import CONFIGS, pose_f32
+    cfg = CONFIGS[cfgname]
+    lg = cfg.log2_n
+    W, H = cfg.width, cfg.height
+    r = rv.StateRender((lg,) * 3, W, H, flags=cfg.flags, atlas=atlas)
+    r.world_build()
+    for s in range(max(cfg.gi_sweeps, 0)):
+        r.gi_update(s)
+    r.sync()
+    ow = check_world_rays_gi(r, rv, oracle, atlas, (lg,) * 3, lg, gi_window=cfg.gi_sweeps >= 0)
+    cam, vp = rv.camera_from_pose(*pose_f32(cfg, pose), W, H)
+    r.frame(cam, vp)
+    check_rows(r, rv, oracle, ow, W, H, cfg.flags, rv.camera_dict(cam, vp), np.random.default_rng(lg + 100))
+    r.close()
+
+
+def test_reference_native_config_draw_cuda(rv, atlas, oracle):
+    """The reference as it ships: 4096 x 512 x 4096 world (include/cumath.cuh:
+    19-21), 1280 x 800 (include/State.hpp:28-29), GI initialised then one
+    UpdateGIData before each drawCUDA (src/main.cpp:119-132), drawCUDA with
+    the c_cam off-by-one (time <- jitterY, jitter <- (0, 0); Appendix R1) and
+    minDist's normalized-coordinate fetch (RV_F_REF_FETCH), camera at the
+    reference defaults (src/Character.cpp:30,45-46)."""
+    import math
+    log2 = (12, 9, 12)
+    W, H = 1280, 800
+    flags = rv.RV_FLAGS_REFERENCE
+    r = rv.StateRender(log2, W, H, flags=flags, atlas=atlas, ref_compat=True)
+    r.world_build()
+    r.update_gi_data()              # frame 0: cells [0, 262144)
+    r.sync()
+    ow = check_world_rays_gi(r, rv, oracle, atlas, log2, 12)
+    f32 = lambda v: float(np.float32(v))
+    cam, vp = rv.camera_from_pose((128.0, 350.0, 128.0), f32(-0.7), f32(-math.pi - 0.3), W, H)
+    d = rv.camera_dict(cam, vp)
+    r.draw_cuda(d["pos"], d["fo"], d["up"], d["ri"], vp, vp, 0.3, 0.7)   # jitterX ignored, time = 0.7
+    rows = check_rows(r, rv, oracle, ow, W, H, flags | rv.RV_F_REF_FETCH, d, np.random.default_rng(7), time=0.7,
+                      nrows=8)
+    assert len(rows) >= 8
+    # how much the R6 fetch matters on this frame: the same rows with exact texel indices (informational)
+    fr = oracle.make_frame(W, H, flags, d, time=0.7)
+    img = r.readback(rv.RV_IMAGE_COLOR)
+    ndiff = sum(int(np.any(oracle.render(ow, fr, y, y + 1, want_stats=False)["rgba"][y] != img[y], axis=-1).sum())
+                for y in rows)
+    print(f"native frame: {ndiff} pixels of {len(rows)} rows differ between the reference fetch and exact texels")
     r.close()
 
 
@@ -105,7 +192,7 @@ def test_fullsize_pipelined_frames(rv, atlas, cfgname):
     k | GI update k+1 | pre-pass k+1) against UpdateGIData + drawCUDA one
     frame at a time on the same full-size world: colour, depth and the GI
     grid bit-identical after 6 frames (the one-at-a-time frames are checked
-    against the oracle by the test above)."""
+    against the oracle by the tests above)."""
     from rvgrt_amd.configs import CONFIGS, pose_f32
     cfg = CONFIGS[cfgname]
     W, H = cfg.width, cfg.height

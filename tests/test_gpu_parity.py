@@ -9,7 +9,7 @@ the fog / Fresnel terms).
 import numpy as np
 import pytest
 
-from conftest import random_rays
+from conftest import Hip as _Hip, random_rays
 
 pytestmark = pytest.mark.gpu
 
@@ -241,6 +241,44 @@ def test_golden_fixtures(rv, atlas):
         r.close()
 
 
+def test_golden_frames(rv, atlas):
+    """The six golden frames of tests/golden (160x96 on the 128^3 world, C1 /
+    C2 / reference flags, poses P0 / P1): MV and depth hashes and the work
+    counters equal the fixture exactly; RGBA8 equals the fixture PNG within
+    the frame tolerance (|d| <= 2 LSB, >= 99.5 % exact; hash equality
+    reported)."""
+    import hashlib
+    import json
+    import os
+    from rvgrt_amd.atlas import decode_png
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    g = json.load(open(os.path.join(gdir, "golden.json")))
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    r = None
+    exact = 0
+    for key, fr in sorted(g["frames"].items()):
+        W, H = (int(v) for v in key.split("_")[1].split("x"))
+        if r is None:
+            r = _gpu_world(rv, atlas, 7, 7, 7, W, H, gi_sweeps=1)
+        pos, yaw, pitch = fr["pose"]
+        cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
+        r.stats_reset()
+        r.frame(cam, vp, flags=fr["flags"] | rv.RV_F_STATS)
+        img = r.readback(rv.RV_IMAGE_COLOR)
+        assert sha(r.readback(rv.RV_IMAGE_MOTION)) == fr["mv"], key
+        assert sha(r.readback(rv.RV_IMAGE_DEPTH)) == fr["depth"], key
+        st = r.stats()
+        for k, v in fr["stats"].items():
+            assert st[k] == v, (key, k, st[k], v)
+        with open(os.path.join(gdir, f"{key}.png"), "rb") as f:
+            want = decode_png(f.read())
+        d = np.abs(img.astype(np.int32) - want.astype(np.int32)).max(axis=2)
+        assert d.max() <= 2 and (d == 0).mean() >= 0.995, key
+        exact += sha(img) == fr["rgba"]
+    print(f"golden frames with identical RGBA8 hash: {exact}/{len(g['frames'])}")
+    r.close()
+
+
 @pytest.mark.parametrize("flags", [0, 8, 7])
 def test_wavefront_equals_per_pixel_path(rv, atlas, flags):
     """The wavefront stages and the per-pixel (megakernel) path are two
@@ -298,34 +336,6 @@ def test_gi_async_update_matches_serial_and_oracle(rv, atlas, oracle_world):
         ow.gi_update(k, first=off, count=min(rays, n - off))
         off = 0 if off + rays >= n else off + rays
     assert np.array_equal(res[1][0], ow.gi)
-
-
-class _Hip:
-    """Streams and device buffers from the HIP runtime the library loaded
-    (the test must not bring in a second runtime through torch)."""
-    def __init__(self):
-        import ctypes as C
-        self.C = C
-        self.L = C.CDLL("libamdhip64.so.7")
-        self.owned = []
-
-    def stream(self):
-        s = self.C.c_void_p()
-        assert self.L.hipStreamCreate(self.C.byref(s)) == 0
-        self.owned.append(("s", s))
-        return s.value
-
-    def malloc(self, n):
-        p = self.C.c_void_p()
-        assert self.L.hipMalloc(self.C.byref(p), self.C.c_size_t(n)) == 0
-        assert self.L.hipMemset(p, 0, self.C.c_size_t(n)) == 0
-        self.owned.append(("m", p))
-        return p.value
-
-    def close(self):
-        self.L.hipDeviceSynchronize()
-        for kind, h in self.owned:
-            (self.L.hipStreamDestroy if kind == "s" else self.L.hipFree)(h)
 
 
 @pytest.mark.parametrize("flags", [8, 7])

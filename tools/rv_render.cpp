@@ -3,7 +3,15 @@
 // star replaces with an offscreen framebuffer dump.  Uses only the C++
 // facade include/StateRender.hpp over the C ABI (no HIP headers).
 //
-//   rv_render [--config c1..c5] [--frames N] [--out frame.ppm] [--atlas texturepack.png]
+//   rv_render [--config c1..c5] [--frames N] [--warmup N] [--out frame.ppm]
+//             [--atlas texturepack.png] [--lg L] [--res WxH] [--flags F]
+//             [--sweeps S] [--gi-per-frame 0|1] [--pose x,y,z,yaw,pitch]
+// --config picks a BASELINE configuration; the other options override its
+// world size, resolution, RV_F_* flags, GI sweeps, per-frame GI update and
+// camera pose (default: the reference's defaults scaled to the world,
+// src/Character.cpp:30,45-46).  Frames go through drawCUDA with the
+// reference's ref_compat settings (Settings defaults).
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -84,17 +92,41 @@ bool decode_png(const std::vector<uint8_t>& f, std::vector<uint8_t>& rgba, int& 
 
 int main(int argc, char** argv) {
     std::string config = "c2", out = "frame.ppm", atlas_path = "rvgrt_amd/assets/texturepack.png";
-    int frames = 60;
+    int frames = 60, warmup = 5;
+    int lg = -1, w = -1, h = -1, flags = -1, sweeps = -2, gpf = -1;
+    float pose[5] = {0, 0, 0, 0, 0};
+    bool have_pose = false;
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string k = argv[i];
-        if (k == "--config") config = argv[i + 1];
-        else if (k == "--frames") frames = std::atoi(argv[i + 1]);
-        else if (k == "--out") out = argv[i + 1];
-        else if (k == "--atlas") atlas_path = argv[i + 1];
+        const char* v = argv[i + 1];
+        if (k == "--config") config = v;
+        else if (k == "--frames") frames = std::atoi(v);
+        else if (k == "--warmup") warmup = std::atoi(v);
+        else if (k == "--out") out = v;
+        else if (k == "--atlas") atlas_path = v;
+        else if (k == "--lg") lg = std::atoi(v);
+        else if (k == "--res") { if (std::sscanf(v, "%dx%d", &w, &h) != 2) { std::fprintf(stderr, "bad --res\n"); return 2; } }
+        else if (k == "--flags") flags = std::atoi(v);
+        else if (k == "--sweeps") sweeps = std::atoi(v);
+        else if (k == "--gi-per-frame") gpf = std::atoi(v);
+        else if (k == "--pose") {
+            if (std::sscanf(v, "%f,%f,%f,%f,%f", &pose[0], &pose[1], &pose[2], &pose[3], &pose[4]) != 5) {
+                std::fprintf(stderr, "bad --pose\n");
+                return 2;
+            }
+            have_pose = true;
+        } else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
-    const Cfg* cfg = nullptr;
-    for (const Cfg& c : kConfigs) if (config == c.name) cfg = &c;
-    if (!cfg) { std::fprintf(stderr, "unknown config %s\n", config.c_str()); return 2; }
+    const Cfg* base = nullptr;
+    for (const Cfg& c : kConfigs) if (config == c.name) base = &c;
+    if (!base) { std::fprintf(stderr, "unknown config %s\n", config.c_str()); return 2; }
+    Cfg cfg_v = *base;
+    if (lg > 0) cfg_v.lg = lg;
+    if (w > 0) { cfg_v.w = w; cfg_v.h = h; }
+    if (flags >= 0) cfg_v.flags = flags;
+    if (sweeps >= -1) cfg_v.sweeps = sweeps;
+    if (gpf >= 0) cfg_v.gi_per_frame = gpf != 0;
+    const Cfg* cfg = &cfg_v;
 
     std::vector<uint8_t> atlas;
     int aw = 0, ah = 0;
@@ -115,19 +147,24 @@ int main(int argc, char** argv) {
         double build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         int n = 1 << cfg->lg;
         rvgrt::mat4 vp;
-        rvgrt::Camera cam = rvgrt::StateRender::cameraFromPose(0.1f * n, std::fmin(0.6f * n, 350.0f), 0.1f * n, -0.7f,
-                                                               (float)(-M_PI - 0.3), cfg->w, cfg->h, &vp);
+        if (!have_pose) {
+            pose[0] = 0.1f * n; pose[1] = std::fmin(0.6f * n, 350.0f); pose[2] = 0.1f * n;
+            pose[3] = -0.7f; pose[4] = (float)(-M_PI - 0.3);
+        }
+        rvgrt::Camera cam = rvgrt::StateRender::cameraFromPose(pose[0], pose[1], pose[2], pose[3], pose[4], cfg->w,
+                                                               cfg->h, &vp);
         rvgrt::mat4 prev = vp;
         auto frame = [&]() {
             if (cfg->gi_per_frame) render.updateGIData();      // renderLoop order (main.cpp:119-132)
             render.drawCUDA(cam.pos, cam.forward, cam.up, cam.right, &vp, &prev, 0.0f, 0.0f);
         };
-        for (int k = 0; k < 5; k++) frame();
+        for (int k = 0; k < warmup; k++) frame();
         render.sync();
         t0 = std::chrono::steady_clock::now();
         for (int k = 0; k < frames; k++) frame();
         render.sync();
-        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / frames;
+        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() /
+                    std::max(frames, 1);
         std::vector<uint8_t> px = render.readbackColor();
         std::FILE* f = std::fopen(out.c_str(), "wb");
         std::fprintf(f, "P6\n%d %d\n255\n", cfg->w, cfg->h);
