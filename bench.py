@@ -82,6 +82,11 @@ def main():
                     help="c1..c5 (default c4: 1024^3, 3840x2160, the reference frame with 2-bounce GI and a GI "
                          "update every frame -- the north star's 1-GPU workload, BASELINE configs[3])")
     ap.add_argument("--pose", default="P0")
+    ap.add_argument("--camera", default="path", choices=["path", "static"],
+                    help="path (default): frames differ -- the reference's jitter sequence as drawCUDA maps it "
+                         "with ref_compat (time), a yaw pan of --pan rad/frame, previous VP per frame; "
+                         "static: one camera for every frame (round 1)")
+    ap.add_argument("--pan", type=float, default=0.0005, help="yaw change per frame of the camera path (rad)")
     ap.add_argument("--tile-px", type=int, default=None,
                     help="screen-tile size of the N>1 shard (default: 16 px without the pre-pass, 32 with it; "
                          "tools/shard_probe.py: C2 at 8 ranks renders its slowest share in 19.6 us/frame at "
@@ -122,7 +127,7 @@ def main():
     import torch
     import rvgrt_amd as rv
     from rvgrt_amd.atlas import load_atlas, write_png
-    from rvgrt_amd.configs import CONFIGS, pose_f32
+    from rvgrt_amd.configs import CONFIGS, camera_path, pose_f32
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -187,14 +192,39 @@ def main():
     log(f"[rank {rank}] world {cfg.n}^3 built in {world_s:.2f}s")
 
     pos, yaw, pitch = pose_f32(cfg, args.pose)
-    cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
+    # ---------------------------------------------------------------- camera path
+    # Every frame differs, as in the reference's renderLoop: Character::Update's jitter sequence, mapped
+    # as drawCUDA maps it with ref_compat (time <- jitterY, jitter 0; src/StateRender.cu:15-29), a yaw
+    # pan of --pan rad per frame, and each frame's previous VP = the frame before's (motion vectors).
+    # frames the run takes from the path: warm-up, timed, the stage-timing pass, 9 latency frames
+    n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if nfl > 1 else min(args.steps, 10)
+    n_path = args.warmup + args.steps + n_stage_frames + 9 + 2
+    pan = args.pan if args.camera == "path" else 0.0
+    path = camera_path((pos, yaw, pitch), W, H, n_path, pan=pan, ref_compat=args.camera == "path")
+    if args.camera == "static":   # the round-1 bench: one camera, time 0, no jitter
+        c0, vp0 = rv.camera_from_pose(pos, yaw, pitch, W, H)
+        path = [rv.frame_desc(c0, vp0)] * (n_path + 1)
+    cursor = [0]            # next frame of the path
+
+    def take(k):
+        a = cursor[0]
+        cursor[0] += k
+        return path[a:a + k], path[a + k]
 
     # ---------------------------------------------------------------- work census
-    # One full frame with counters on: rays per frame and algorithmic bytes.
+    # Frames with counters on: rays per frame and algorithmic bytes, the mean
+    # over 8 frames spread over the timed part of the path.
+    census = np.linspace(args.warmup, args.warmup + max(args.steps - 1, 0), 8).astype(int)
     r.stats_reset()
-    r.frame(cam, vp, flags=flags | rv.RV_F_STATS)
-    st_all = r.stats(-1)
-    st_stage = {name: r.stats(k) for k, name in enumerate(rv._lib.STAGES)}
+    for i in census:
+        d = path[i]
+        r.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time,
+                jx=d.jitter_x, jy=d.jitter_y, flags=flags | rv.RV_F_STATS)
+
+    def mean_stats(st):
+        return {k: int(round(v / len(census))) for k, v in st.items()}
+    st_all = mean_stats(r.stats(-1))
+    st_stage = {name: mean_stats(r.stats(k)) for k, name in enumerate(rv._lib.STAGES)}
     rays_per_frame = st_all["traces"]
     gi_stats = None
     if gi_per_frame:   # one UpdateGIData with step counters on: the GI update's algorithmic bytes
@@ -274,7 +304,13 @@ def main():
 
     def run_native(k):
         r.set_stream(stream.cuda_stream)
-        r.render_frames(k, cam, vp, flags=flags, gi_per_frame=gi_per_frame, comm=comm)
+        seq, nxt = take(k)
+        r.render_frame_seq(seq, next_desc=nxt, flags=flags, gi_per_frame=gi_per_frame, comm=comm)
+
+    def frame_args():
+        d = take(1)[0][0]
+        return (d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp)), \
+            {"time": d.time, "jx": d.jitter_x, "jy": d.jitter_y, "flags": flags}
 
     def issue_gather(b):
         if args.dist_backend == "nccl":
@@ -299,11 +335,12 @@ def main():
         k = frame_no[0]
         frame_no[0] += 1
         s = streams[0] if serial[0] else streams[k % nfl]
+        fa, fk = frame_args()
         if world_size == 1:
             r.set_stream(s.cuda_stream)
             if gi_per_frame:
                 r.update_gi_data()   # renderLoop: UpdateGIData before drawCUDA
-            r.frame(cam, vp, flags=flags)
+            r.frame(*fa, **fk)
             return
         b = k % nbuf
         with torch.cuda.stream(s):
@@ -311,7 +348,8 @@ def main():
             if gi_per_frame:
                 r.update_gi_data()
             r.bind_tile_buffer(tbufs[b].data_ptr(), tbufs[b].numel())
-            r.frame_tiles(cam, vp, my_tiles, tile_px=T, flags=flags)
+            r.frame_tiles(fa[0], fa[1], my_tiles, tile_px=T, prev_vp=fa[2], time=fk["time"], jx=fk["jx"],
+                          jy=fk["jy"], flags=flags)
             work = issue_gather(b)   # the gather waits for this frame's render on stream s
         pending.append((work, b, s))
         if nfl == 1 and len(pending) > 1:
@@ -359,7 +397,8 @@ def main():
     stage_fpl = {name: fpl for name in rv._lib.STAGES}
     if gi_groups:
         stage_fpl["pp_primary"] = nfl
-    n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if grouped else min(args.steps, 10)
+    if not grouped:
+        n_stage_frames = min(args.steps, 10)
     serial[0] = True
     r.timing_enable(2 * n_stage_frames + 2)
     if native:
@@ -393,7 +432,9 @@ def main():
     gather_check = None
     if world_size > 1 and rank == 0:   # the gathered frame must equal a one-GPU frame
         tiled = r.readback(rv.RV_IMAGE_COLOR).copy()
-        r.frame(cam, vp, flags=flags)
+        d = path[cursor[0] - 1]   # the last frame rendered
+        r.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time, jx=d.jitter_x,
+                jy=d.jitter_y, flags=flags)
         full = r.readback(rv.RV_IMAGE_COLOR)
         nbad = int(np.count_nonzero(np.any(tiled != full, axis=-1)))
         gather_check = "exact" if nbad == 0 else f"{nbad} pixels differ"
@@ -456,7 +497,7 @@ def main():
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and world_size == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(r, cfg, cam, vp, flags, atlas, args.cpu_seconds)
+        cpu = cpu_baseline(r, cfg, path[args.warmup], flags, atlas, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -475,6 +516,10 @@ def main():
             "dtype": "f32",
             "data": "synthetic: procedural world from the reference Evaluate (seed 0), camera pose "
                     f"{args.pose} (reference defaults), random-free",
+            "camera": ("per-frame: yaw pan %g rad/frame from the pose, the reference jitter sequence as "
+                       "drawCUDA maps it with ref_compat (time <- jitterY), previous VP per frame; rays_per_frame "
+                       "= mean of 8 census frames of the timed path" % pan) if args.camera == "path"
+                      else "static: one camera, time 0, no jitter",
             "config": {"workload": cfg.name, "world": f"{cfg.n}^3", "resolution": f"{W}x{H}",
                        "flags": flags, "gi_sweeps": cfg.gi_sweeps, "gi_update_per_frame": gi_per_frame,
                        "parallelism": f"screen-tiles {T}px x{world_size}" if world_size > 1 else "single-gpu"},
@@ -504,7 +549,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
+def cpu_baseline(r, cfg, d, flags, atlas, budget_s):
     """The CPU oracle (scalar DDA restatement, oracle/rv_oracle.c) on the host
     cores: same world (exported from the GPU; bit-identical to the oracle's
     own build, tests/test_gpu_parity.py), same camera and features, the frame
@@ -522,7 +567,8 @@ def cpu_baseline(r, cfg, cam, vp, flags, atlas, budget_s):
     w.bits[:] = r.world_export(rv.RV_WORLD_BITS)
     w.csdf[:] = r.world_export(rv.RV_WORLD_CSDF)
     w.gi[:] = r.world_export(rv.RV_WORLD_GI)
-    fr = O.make_frame(cfg.width, cfg.height, flags, rv.camera_dict(cam, vp))
+    fr = O.make_frame(cfg.width, cfg.height, flags, rv.camera_dict(d.cam, np.ctypeslib.as_array(d.vp)), time=d.time,
+                      jx=d.jitter_x, jy=d.jitter_y, pvp=np.ctypeslib.as_array(d.prev_vp))
     H = cfg.height
     stride = 16 if cfg.width * cfg.height > 1920 * 1080 else 1
     rows_all = np.arange(0, H, stride, dtype=np.int32)

@@ -39,6 +39,11 @@ class rv_camera(C.Structure):
                 ("up", C.c_float * 3), ("mul", C.c_float * 2), ("add", C.c_float * 2)]
 
 
+class rv_frame_desc(C.Structure):
+    _fields_ = [("cam", rv_camera), ("vp", C.c_float * 16), ("prev_vp", C.c_float * 16),
+                ("time", C.c_float), ("jitter_x", C.c_float), ("jitter_y", C.c_float)]
+
+
 class rv_hit(C.Structure):
     _fields_ = [("pos", C.c_float * 3), ("normal", C.c_float * 3), ("u", C.c_float),
                 ("v", C.c_float), ("hit", C.c_int32), ("undef", C.c_int32),
@@ -105,6 +110,7 @@ SIGNATURES = [
     ("rv_comm_destroy", None, [P]),
     ("rv_set_tile_shard", I32, [P, I32, I32, I32]),
     ("rv_render_frames", I32, [P, I32, C.POINTER(rv_camera), P, P, F, F, F, I32, I32, P]),
+    ("rv_render_frame_seq", I32, [P, I32, C.POINTER(rv_frame_desc), C.POINTER(rv_frame_desc), I32, I32, P]),
 ]
 
 _lib = None

@@ -64,3 +64,39 @@ def pose_f32(cfg: RenderConfig, which="P0"):
     import numpy as np
     pos, yaw, pitch = cfg.pose(which)
     return (tuple(float(np.float32(v)) for v in pos), float(np.float32(yaw)), float(np.float32(pitch)))
+
+
+# src/Character.cpp:9-15: the TAA jitter table; Character::Update uses
+# entry frameCount % 8, scaled by 0.5 (:101-102).
+JITTER_SEQUENCE = ((-1 / 8, -1 / 8), (1 / 8, 3 / 8), (5 / 8, -3 / 8), (-3 / 8, 5 / 8),
+                   (-7 / 8, -5 / 8), (3 / 8, 7 / 8), (7 / 8, -7 / 8), (-5 / 8, 1 / 8))
+
+
+def camera_path(pose, width, height, frames, start=0, pan=0.0005, ref_compat=True):
+    """The per-frame inputs renderLoop hands drawCUDA (src/main.cpp:119-132)
+    for a camera panning `pan` rad of yaw per frame from `pose` ((pos, yaw,
+    pitch) as RenderConfig.pose returns it): frame f's camera and unjittered
+    VP from Character::Update, the previous frame's VP, and the jitter
+    sequence -- mapped as drawCUDA maps it with ref_compat (time <- jitterY,
+    jitter <- (0, 0)), or applied as ray jitter without.
+    Returns frames + 1 rv_frame_desc: frames start..start+frames-1 and the
+    one after them (rv_render_frame_seq's `next`)."""
+    import numpy as np
+    from .render import camera_from_pose, frame_desc
+    pos, yaw, pitch = pose
+
+    def cam(f):
+        y = float(np.float32(np.float32(yaw) + np.float32(pan) * np.float32(f)))
+        return camera_from_pose(pos, y, float(np.float32(pitch)), width, height)
+
+    out = []
+    _, prev = cam(start - 1)
+    for f in range(start, start + frames + 1):
+        c, vp = cam(f)
+        jx, jy = (float(np.float32(v * 0.5)) for v in JITTER_SEQUENCE[f % 8])
+        if ref_compat:
+            out.append(frame_desc(c, vp, prev, time=jy, jx=0.0, jy=0.0))
+        else:
+            out.append(frame_desc(c, vp, prev, time=0.0, jx=jx, jy=jy))
+        prev = vp
+    return out

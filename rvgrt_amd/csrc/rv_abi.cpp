@@ -144,6 +144,19 @@ struct rv_ctx {
     int shard_px = 0, shard_rank = 0, shard_n = 0, shard_max = 0;
     std::vector<int32_t> shard_ids, shard_all;
     uint64_t world_ver = 1;        // bumped by every world/GI write (mark_world)
+    uint64_t geom_ver = 1;         // bumped by every voxel-bits / CSDF write (what the pre-pass reads)
+    // Pipelined loop: the next frame's GI update and pre-pass computed by the last launch of a call and
+    // kept for the next call (rv_render_frame_seq).  gi: update `carry_fr` of [carry_first, +count) in
+    // gi_tmp (or this rank's shard in pipe_gi_stage), not yet copied back; pp: pre-pass of the camera
+    // `carry_key` in pipe_half[carry_half].
+    bool carry_gi = false, carry_pp = false;
+    uint32_t carry_fr = 0; uint64_t carry_first = 0, carry_count = 0, carry_world = 0, carry_geom = 0;
+    uint64_t carry_chunk = 0; int carry_n = 0, carry_r = 0, carry_half = 0;
+    float carry_key[24] = {};
+    int pipe_carry = 1;            // RV_PIPE_CARRY
+    // per-frame camera table of batched launches (rv_render_frame_seq): device copy, pinned staging
+    FrameCam* cam_dev = nullptr; FrameCam* cam_host = nullptr; size_t cam_cap = 0;
+    hipEvent_t cam_ev = nullptr; bool cam_pending = false;
     uint64_t gi_swapped_at = 0;    // frame_seq at the last GI buffer flip: older frames read gi_tmp
     hipStream_t world_stream = nullptr;   // stream ev_world was recorded on
     int cur_slot = 0;
@@ -336,6 +349,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_GI_PRIO")) c->gi_low_prio = atoi(e);
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
+    if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
     if (const char* e = getenv("RV_GATHER_BPP")) c->gather_bpp = atoi(e) == 4 ? 4 : 3;
     if (const char* e = getenv("RV_PIPE_ORDER")) {   // a permutation of the parts, else the default
         const uint32_t o = (uint32_t)strtoul(e, nullptr, 16);
@@ -433,6 +447,9 @@ void rv_destroy(rv_ctx* c) {
     if (c->comm_stream) hipStreamDestroy(c->comm_stream);
     if (c->ev_loop) hipEventDestroy(c->ev_loop);
     if (c->ev_world) hipEventDestroy(c->ev_world);
+    hipFree(c->cam_dev);
+    if (c->cam_host) hipHostFree(c->cam_host);
+    if (c->cam_ev) hipEventDestroy(c->cam_ev);
     if (c->ev_gi_done) hipEventDestroy(c->ev_gi_done);
     delete c;
 }
@@ -552,6 +569,7 @@ rv_status rv_set_gi_async(rv_ctx* c, int32_t on) {
 rv_status rv_set_pipeline(rv_ctx* c, int32_t on) {
     if (!c) return RV_ERR_INVALID;
     c->pipe = on != 0;
+    c->carry_gi = c->carry_pp = false;
     return RV_OK;
 }
 
@@ -573,6 +591,7 @@ rv_status rv_sync(rv_ctx* c) {
 rv_status rv_csdf_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
+    c->geom_ver++;
     uint64_t n = n_csdf(c);
     uint8_t *t0 = nullptr, *t1 = nullptr;
     HIP_TRY(c, hipMallocAsync((void**)&t0, n, c->stream));
@@ -597,6 +616,7 @@ rv_status rv_gi_init(rv_ctx* c) {
 rv_status rv_world_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
+    c->geom_ver++;
     launch_fill_bricks(c->stream, c->brick, current_world(c), c->cfg.seed_x, c->cfg.seed_z);
     LAUNCH_CHECK(c);
     rv_status s = rv_csdf_build(c);
@@ -610,6 +630,7 @@ rv_status rv_world_build(rv_ctx* c) {
 rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t bytes) {
     if (!c || !host) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
+    if (kind != RV_WORLD_GI) c->geom_ver++;
     if (kind == RV_WORLD_BITS) {
         if (bytes != n_bits_words(c) * 4) return fail(c, RV_ERR_INVALID, "bits size mismatch");
         uint32_t* d = nullptr;
@@ -758,6 +779,62 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
     f.wtrace = c->wtrace;
     f.nbatch = 1;
     return f;
+}
+
+static FrameParams make_params_d(rv_ctx* c, const rv_frame_desc& d, int32_t flags) {
+    return make_params(c, &d.cam, d.vp, d.prev_vp, d.time, d.jitter_x, d.jitter_y, flags);
+}
+
+// A frame sequence: desc k = d[k * stride] (stride 0: one camera for every
+// frame); after() = the frame that follows the sequence.
+struct Seq {
+    const rv_frame_desc* d = nullptr;
+    int stride = 0, n = 0;
+    const rv_frame_desc* next = nullptr;
+    const rv_frame_desc& at(int k) const { return d[(size_t)k * stride]; }
+    const rv_frame_desc& after() const { return next ? *next : at(n - 1); }
+    bool uniform(int k0, int k1) const {   // frames [k0, k1) share one camera
+        if (stride == 0) return true;
+        for (int k = k0 + 1; k < k1; k++)
+            if (std::memcmp(&at(k), &at(k0), sizeof(rv_frame_desc)) != 0) return false;
+        return true;
+    }
+};
+
+static FrameCam frame_cam(const rv_frame_desc& d) {
+    FrameCam fc{};
+    fc.pos = host_v(d.cam.pos[0], d.cam.pos[1], d.cam.pos[2]);
+    fc.fo = host_v(d.cam.forward[0], d.cam.forward[1], d.cam.forward[2]);
+    fc.ri = host_v(d.cam.right[0], d.cam.right[1], d.cam.right[2]);
+    fc.up = host_v(d.cam.up[0], d.cam.up[1], d.cam.up[2]);
+    fc.time = d.time; fc.jx = d.jitter_x; fc.jy = d.jitter_y;
+    for (int i = 0; i < 16; i++) { fc.vp[i] = d.vp[i]; fc.pvp[i] = d.prev_vp[i]; }
+    return fc;
+}
+
+// Uploads the cameras of all frames of a sequence (batched launches index it
+// from their first frame) on stream st; returns the device table.  The
+// pinned staging buffer is reused only after its last upload has executed.
+static rv_status upload_cams(rv_ctx* c, const Seq& q, hipStream_t st, const FrameCam** out) {
+    const size_t n = (size_t)q.n;
+    if (c->cam_pending) HIP_TRY(c, hipEventSynchronize(c->cam_ev));
+    if (n > c->cam_cap) {
+        HIP_TRY(c, hipDeviceSynchronize());   // kernels of earlier calls may still read the old table
+        hipFree(c->cam_dev);
+        if (c->cam_host) hipHostFree(c->cam_host);
+        c->cam_dev = nullptr; c->cam_host = nullptr; c->cam_cap = 0;
+        const size_t cap = std::max<size_t>(n, 256);
+        HIP_TRY(c, hipMalloc(&c->cam_dev, cap * sizeof(FrameCam)));
+        HIP_TRY(c, hipHostMalloc(&c->cam_host, cap * sizeof(FrameCam), hipHostMallocDefault));
+        c->cam_cap = cap;
+    }
+    if (!c->cam_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->cam_ev, hipEventDisableTiming));
+    for (size_t k = 0; k < n; k++) c->cam_host[k] = frame_cam(q.at((int)k));
+    HIP_TRY(c, hipMemcpyAsync(c->cam_dev, c->cam_host, n * sizeof(FrameCam), hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipEventRecord(c->cam_ev, st));
+    c->cam_pending = true;
+    *out = c->cam_dev;
+    return RV_OK;
 }
 
 // Enqueue the frame's stages, recording a start event per stage when timing
@@ -1330,8 +1407,8 @@ static rv_status bset_publish(rv_ctx* c, const BatchSet& lb, size_t li, bool all
 // a group of B frames (one launch, frame index in the grid); then frame by
 // frame the GI update (kernel overlapping the previous render on the GI
 // stream) and the render, which reads its frame's half-res images.
-static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
-                                  const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S) {
+static rv_status render_gi_groups(rv_ctx* c, const Seq& q, int32_t flags, hipStream_t S) {
+    const int frames = q.n;
     const int B = (int)c->slots.size();
     const int W = c->cfg.width, H = c->cfg.height;
     const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
@@ -1342,16 +1419,20 @@ static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* ca
     slot_load(c, 0);
     c->stream = S;
     if (rv_status ws = wait_all_frames(c)) return ws;   // frames of earlier calls, the last world write
+    const FrameCam* cams = nullptr;
+    if (!q.uniform(0, frames))
+        if (rv_status us = upload_cams(c, q, S, &cams)) return us;
     int done = 0, last = 0;
     while (done < frames) {
         const int nb = std::min(B, frames - done);
-        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+        FrameParams f = make_params_d(c, q.at(done), flags);
         f.nbatch = (uint32_t)nb;
+        if (cams) f.cams = cams + done;
         f.hdist = bs.hdist; f.hshadow = bs.hshadow; f.bs_half = hbytes;
         if (rv_status rs = run_stages(c, f, false, 1)) return rs;
         for (int j = 0; j < nb; j++) {
             if (rv_status gs = rv_update_gi_data(c)) return gs;
-            FrameParams g = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+            FrameParams g = make_params_d(c, q.at(done + j), flags);
             g.hdist = reinterpret_cast<float*>(reinterpret_cast<char*>(bs.hdist) + (size_t)j * hbytes);
             g.hshadow = reinterpret_cast<float*>(reinterpret_cast<char*>(bs.hshadow) + (size_t)j * hbytes);
             g.color = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(bs.color) + (size_t)j * cstride);
@@ -1392,9 +1473,22 @@ static rv_status render_gi_groups(rv_ctx* c, int32_t frames, const rv_camera* ca
 #endif
 constexpr uint32_t PIPE_WSTAT_N = 32, PIPE_WSTAT_MAXB = 1u << 18;   // launches, workgroups per launch
 
-static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
-                                const float* pvp16, float time, float jx, float jy, int32_t flags, hipStream_t S,
-                                rv_comm* comm) {
+// What a kept pre-pass was computed for: the camera fields the pre-pass
+// reads, the pre-pass flag and the tile shard (its footprints).
+static void pp_key(const rv_ctx* c, const rv_frame_desc& d, int32_t flags, float (&k)[24]) {
+    std::memset(k, 0, sizeof(k));
+    for (int i = 0; i < 3; i++) {
+        k[i] = d.cam.pos[i]; k[3 + i] = d.cam.forward[i]; k[6 + i] = d.cam.right[i]; k[9 + i] = d.cam.up[i];
+    }
+    k[12] = d.jitter_x; k[13] = d.jitter_y;
+    uint32_t h = 2166136261u;   // FNV-1a of the shard's tile ids
+    for (int32_t t : c->shard_ids) h = (h ^ (uint32_t)t) * 16777619u;
+    const int32_t iv[6] = {flags & RV_F_PREPASS, c->shard_n, c->shard_rank, c->shard_px, (int32_t)h, 0};
+    std::memcpy(&k[14], iv, sizeof(iv));
+}
+
+static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStream_t S, rv_comm* comm) {
+    const int frames = q.n;
     const int W = c->cfg.width, H = c->cfg.height;
     const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
     const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
@@ -1409,16 +1503,16 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
     const uint64_t n = n_gi(c), rays = c->cfg.gi_rays_per_frame;
     const uint64_t chunk = shard_gi ? (rays + N - 1) / N : 0;   // GI cells per rank (all-gather unit)
     for (auto& ph : c->pipe_half)
-        for (int q = 0; q < 2; q++)
-            if (!ph[q]) HIP_TRY(c, hipMalloc(&ph[q], hbytes));
+        for (int q2 = 0; q2 < 2; q2++)
+            if (!ph[q2]) HIP_TRY(c, hipMalloc(&ph[q2], hbytes));
     if (!c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
     if (tiles && (c->pipe_slice != slice || c->pipe_gbytes != (root ? slice * N : 0))) {
         HIP_TRY(c, hipDeviceSynchronize());
-        for (int q = 0; q < 2; q++) {
-            hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]);
-            c->pipe_tbuf[q] = nullptr; c->pipe_gbuf[q] = nullptr;
-            HIP_TRY(c, hipMalloc(&c->pipe_tbuf[q], slice ? slice : 1));
-            if (root) HIP_TRY(c, hipMalloc(&c->pipe_gbuf[q], slice * N));
+        for (int b = 0; b < 2; b++) {
+            hipFree(c->pipe_tbuf[b]); hipFree(c->pipe_gbuf[b]);
+            c->pipe_tbuf[b] = nullptr; c->pipe_gbuf[b] = nullptr;
+            HIP_TRY(c, hipMalloc(&c->pipe_tbuf[b], slice ? slice : 1));
+            if (root) HIP_TRY(c, hipMalloc(&c->pipe_gbuf[b], slice * N));
         }
         c->pipe_slice = slice; c->pipe_gbytes = root ? slice * N : 0;
     }
@@ -1426,6 +1520,7 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         HIP_TRY(c, hipDeviceSynchronize());
         hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);
         c->pipe_gi_stage = nullptr; c->pipe_gi_all = nullptr;
+        c->carry_gi = false;   // the kept shard lived in the old stage buffer
         HIP_TRY(c, hipMalloc(&c->pipe_gi_stage, chunk * 4));
         HIP_TRY(c, hipMalloc(&c->pipe_gi_all, chunk * N * 4));
         c->pipe_chunk = chunk; c->pipe_chunk_n = N;
@@ -1444,14 +1539,32 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         if (rv_status us = upload_ids(c, c->untile_ids, c->shard_all.data(), (int)c->shard_all.size(), nullptr)) return us;
         if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
     }
-    auto next_range = [&](uint32_t& fr, uint64_t& first, uint64_t& count) {   // rv_update_gi_data's walk
+    auto peek_range = [&](uint32_t& fr, uint64_t& first, uint64_t& count) {   // rv_update_gi_data's next window
         fr = c->gi_frame;
         first = c->gi_offset;
         count = first + rays > n ? n - first : rays;
+    };
+    auto next_range = [&](uint32_t& fr, uint64_t& first, uint64_t& count) {   // ... and advance to the one after
+        peek_range(fr, first, count);
         c->gi_frame++;
         if (c->gi_offset + rays >= n) c->gi_offset = 0;   // src/CoarseArray.cu:392-394
         else c->gi_offset += rays;
     };
+    // work the previous call's last launch did for this call's first frame
+    float key0[24];
+    pp_key(c, q.at(0), flags, key0);
+    uint32_t fr = 0;
+    uint64_t first = 0, count = 0;
+    peek_range(fr, first, count);
+    const bool use_gi = c->pipe_carry && c->carry_gi && c->carry_world == c->world_ver &&
+                        c->carry_n == (shard_gi ? N : 0) && c->carry_r == (shard_gi ? R : 0) &&
+                        c->carry_chunk == chunk && c->carry_fr == fr && c->carry_first == first &&
+                        c->carry_count == count;
+    const bool use_pp = c->pipe_carry && c->carry_pp && c->carry_geom == c->geom_ver &&
+                        std::memcmp(c->carry_key, key0, sizeof(key0)) == 0;
+    const int base = use_pp ? c->carry_half : 0;   // frame k's half-res images: pipe_half[(base + k) & 1]
+    c->carry_gi = c->carry_pp = false;
+    auto half = [&](int k) { return (base + k) & 1; };
     auto tile_params = [&](FrameParams& f, int k) {
         if (!tiles) return;
         f.tiles = c->tiles.d; f.ntiles = (int)c->shard_ids.size(); f.tile_px = T; f.tiles_x = (W + T - 1) / T;
@@ -1460,15 +1573,23 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
     };
     const World w = current_world(c);
     unsigned long long* cnt_gi = c->counters + (size_t)ST_GI * NCNT;
-    uint32_t fr = 0;
-    uint64_t first = 0, count = 0;
-    next_range(fr, first, count);   // frame 0's update: every rank the whole window (identical grids)
-    launch_gi_update(S, c->gi, c->gi_tmp, w, sun_dir(), fr, first, count, cnt_gi, c->gi_stats);
-    LAUNCH_CHECK(c);
-    HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
-    {
-        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
-        f.hdist = c->pipe_half[0][0]; f.hshadow = c->pipe_half[0][1];
+    next_range(fr, first, count);   // frame 0's update: every rank the whole window (identical grids) ...
+    if (!use_gi) {
+        launch_gi_update(S, c->gi, c->gi_tmp, w, sun_dir(), fr, first, count, cnt_gi, c->gi_stats);
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+    } else if (xchg) {   // ... or kept from the previous call: this rank's share, exchanged now
+        NCCL_TRY(c, g_rccl.all_gather(c->pipe_gi_stage, c->pipe_gi_all, chunk, ncclUint32, comm->comm,
+                                      c->comm_stream));
+        HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
+        HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[1], 0));
+        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->pipe_gi_all, count * 4, hipMemcpyDeviceToDevice, S));
+    } else if (!probe) {
+        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+    }
+    if (!use_pp) {
+        FrameParams f = make_params_d(c, q.at(0), flags);
+        f.hdist = c->pipe_half[half(0)][0]; f.hshadow = c->pipe_half[half(0)][1];
         f.counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
         tile_params(f, 0);
         if (tiles) launch_prepass_tiles(S, w, f); else launch_prepass(S, w, f);
@@ -1483,9 +1604,12 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         return RV_OK;
     };
     for (int k = 0; k < frames; k++) {
-        const bool more = k + 1 < frames;
-        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
-        f.hdist = c->pipe_half[k & 1][0]; f.hshadow = c->pipe_half[k & 1][1];
+        const bool last = k + 1 == frames;
+        // every launch also runs the next frame's update and pre-pass; the last launch's are kept for the
+        // next call (RV_PIPE_CARRY=0: the last launch renders only)
+        const bool more = !last || c->pipe_carry;
+        FrameParams f = make_params_d(c, q.at(k), flags);
+        f.hdist = c->pipe_half[half(k)][0]; f.hshadow = c->pipe_half[half(k)][1];
         f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
         tile_params(f, k);
         if (xchg && k >= 2)   // tile buffer k & 1 is free once frame k-2's gather has read it
@@ -1494,16 +1618,23 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         p.gi_prev = c->gi;
         uint64_t mine = 0, mfirst = 0;
         if (more) {
-            next_range(p.gi_frame, first, count);
+            if (last) peek_range(p.gi_frame, first, count);
+            else next_range(p.gi_frame, first, count);
             mfirst = first; mine = count;
             if (shard_gi) {
                 mfirst = first + std::min<uint64_t>(count, (uint64_t)R * chunk);
                 mine = std::min<uint64_t>(chunk, first + count - mfirst);
             }
+            const rv_frame_desc& nd = last ? q.after() : q.at(k + 1);
+            p.pp_pos = host_v(nd.cam.pos[0], nd.cam.pos[1], nd.cam.pos[2]);
+            p.pp_fo = host_v(nd.cam.forward[0], nd.cam.forward[1], nd.cam.forward[2]);
+            p.pp_ri = host_v(nd.cam.right[0], nd.cam.right[1], nd.cam.right[2]);
+            p.pp_up = host_v(nd.cam.up[0], nd.cam.up[1], nd.cam.up[2]);
+            p.pp_jx = nd.jitter_x; p.pp_jy = nd.jitter_y;
         }
         p.gi_first = mfirst; p.gi_count = mine;
         p.gi_next = shard_gi ? c->pipe_gi_stage : c->gi_tmp + first;
-        p.pp_hdist = c->pipe_half[(k + 1) & 1][0]; p.pp_hshadow = c->pipe_half[(k + 1) & 1][1];
+        p.pp_hdist = c->pipe_half[half(k + 1)][0]; p.pp_hshadow = c->pipe_half[half(k + 1)][1];
         p.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
         p.gi_counters = cnt_gi;
         const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, mine) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
@@ -1533,10 +1664,11 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
             c->ev_used[c->timing_n] = 2;
             c->timing_n++;
         }
+        const bool apply = more && !last;   // this launch's update is frame k+1's: apply it now
         if (xchg) {
             HIP_TRY(c, hipEventRecord(c->pipe_ev[0], S));   // frame k rendered, shard k+1 computed
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->pipe_ev[0], 0));
-            if (more) {   // the update's cells from every rank, then the copy-back on S
+            if (apply) {   // the update's cells from every rank, then the copy-back on S
                 NCCL_TRY(c, g_rccl.all_gather(c->pipe_gi_stage, c->pipe_gi_all, chunk, ncclUint32, comm->comm,
                                               c->comm_stream));
                 HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
@@ -1549,9 +1681,9 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
                                           c->comm_stream));
             NCCL_TRY(c, g_rccl.group_start());
             if (root) {
-                for (int q = 1; q < N; q++)
-                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(c->pipe_gbuf[k & 1]) + (size_t)q * slice, slice,
-                                            ncclUint8, q, comm->comm, c->comm_stream));
+                for (int r = 1; r < N; r++)
+                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(c->pipe_gbuf[k & 1]) + (size_t)r * slice, slice,
+                                            ncclUint8, r, comm->comm, c->comm_stream));
             } else {
                 NCCL_TRY(c, g_rccl.send(c->pipe_tbuf[k & 1], slice, ncclUint8, 0, comm->comm, c->comm_stream));
             }
@@ -1560,13 +1692,22 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
             if (root && k >= 1)   // frame k-1, whose gather overlapped this launch
                 if (rv_status us = untile(k - 1)) return us;
         } else {
-            if (more && !probe)
+            if (apply && !probe)
                 HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
             if (tiles && N == 1) {   // one rank: assemble locally
                 launch_untile(S, c->pipe_tbuf[k & 1], c->untile_ids.d, (int)c->shard_all.size(), T, tiles_x, W, H,
                               c->color, c->color_pitch, c->shard_max, 1, 0, bpp);
                 LAUNCH_CHECK(c);
             }
+        }
+        if (last && more) {   // keep the next frame's update and pre-pass for the next call
+            c->carry_gi = true;
+            c->carry_fr = p.gi_frame; c->carry_first = first; c->carry_count = count;
+            c->carry_n = shard_gi ? N : 0; c->carry_r = shard_gi ? R : 0; c->carry_chunk = chunk;
+            c->carry_pp = true;
+            c->carry_half = half(k + 1);
+            c->carry_geom = c->geom_ver;
+            pp_key(c, q.after(), flags, c->carry_key);
         }
         if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
             c->frames_since_order = 0;
@@ -1589,10 +1730,11 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
         HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[0], 0));
     }
     // the last frame's half-res images become the slot's (rv_readback)
-    const int lk = (frames - 1) & 1;
+    const int lk = half(frames - 1);
     HIP_TRY(c, hipMemcpyAsync(c->hdist, c->pipe_half[lk][0], hbytes, hipMemcpyDeviceToDevice, S));
     HIP_TRY(c, hipMemcpyAsync(c->hshadow, c->pipe_half[lk][1], hbytes, hipMemcpyDeviceToDevice, S));
     if (rv_status ms = mark_world(c)) return ms;
+    c->carry_world = c->world_ver;   // the kept update is valid until the next world/GI write
     FrameSlot& s0 = c->slots[0];
     HIP_TRY(c, hipEventRecord(s0.done, S));
     s0.pending = true;
@@ -1605,9 +1747,9 @@ static rv_status render_gi_pipe(rv_ctx* c, int32_t frames, const rv_camera* cam,
 // one RCCL gather of the group's packed tiles and one untile.  Group j runs
 // on stream j & 1 with batch set j & 1 and frame slot j & 1's scheduling
 // state, so group j+1 fills group j's tail while group j is gathered.
-static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16,
-                                const float* pvp16, float time, float jx, float jy, int32_t flags, rv_comm* comm,
-                                bool own0, hipStream_t caller, size_t slice) {
+static rv_status render_batches(rv_ctx* c, const Seq& q, int32_t flags, rv_comm* comm, bool own0, hipStream_t caller,
+                                size_t slice) {
+    const int frames = q.n;
     const int B = (int)c->slots.size();
     const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
     const int W = c->cfg.width, H = c->cfg.height, T = c->shard_px;
@@ -1641,6 +1783,11 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
         for (const FrameSlot& sl : c->slots)
             if (sl.pending) HIP_TRY(c, hipStreamWaitEvent(x, sl.done, 0));
     }
+    const FrameCam* cams = nullptr;   // per-frame cameras (uploaded on the caller's stream, before the groups)
+    if (!q.uniform(0, frames))
+        if (rv_status us = upload_cams(c, q, caller, &cams)) return us;
+    HIP_TRY(c, hipEventRecord(c->ev_loop, caller));
+    for (hipStream_t x : S) HIP_TRY(c, hipStreamWaitEvent(x, c->ev_loop, 0));
     int done = 0, last_nb = 0, last = 0;
     int prev_k = -1, prev_nb = 0;   // root: group gathered but not yet assembled
     auto untile_group = [&](int kk, int nbb) -> rv_status {
@@ -1652,14 +1799,17 @@ static rv_status render_batches(rv_ctx* c, int32_t frames, const rv_camera* cam,
         return RV_OK;
     };
     for (int j = 0; done < frames; j++) {
-        const int nb = std::min(B, frames - done), k = j & 1;
+        // the remaining frames in equal groups of at most B (20 frames at B = 16: 10 + 10, not 16 + 4)
+        const int groups = (frames - done + B - 1) / B;
+        const int nb = (frames - done + groups - 1) / groups, k = j & 1;
         BatchSet& bs = c->bsets[k];
         c->stream = S[k];
         slot_save(c);
         slot_load(c, k);
         if (bs.pending && tiles && !root) HIP_TRY(c, hipStreamWaitEvent(S[k], bs.gathered, 0));   // tile buffer reuse
-        FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
+        FrameParams f = make_params_d(c, q.at(done), flags);
         f.nbatch = (uint32_t)nb;
+        if (cams) f.cams = cams + done;
         f.color = bs.color; f.color_pitch = c->own_color_pitch; f.bs_color = cstride;
         f.mv = bs.mv; f.mv_pitch = c->own_mv_pitch; f.bs_mv = mstride;
         f.depth = bs.depth; f.depth_pitch = c->own_depth_pitch; f.bs_depth = dstride;
@@ -1812,9 +1962,8 @@ rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nr
     return RV_OK;
 }
 
-rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16, const float* pvp16,
-                           float time, float jx, float jy, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
-    if (!c || !cam || frames < 0) return RV_ERR_INVALID;
+static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
+    const int frames = q.n;
     if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_render_frames before world");
     if (comm && (c->shard_n != comm->nranks || c->shard_rank != comm->rank))
         return fail(c, RV_ERR_INVALID, "tile shard does not match the communicator");
@@ -1865,14 +2014,14 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
     for (hipStream_t fs : c->fstreams) HIP_TRY(c, hipStreamWaitEvent(fs, c->ev_loop, 0));
     if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_loop, 0));
     if (!gi_per_frame && n > 1 && c->megakernel && frames > 0) {
-        st = render_batches(c, frames, cam, vp16, pvp16, time, jx, jy, flags, comm, own0, caller, slice);
+        st = render_batches(c, q, flags, comm, own0, caller, slice);
         c->ext_tilebuf = saved_ext; c->ext_tilebuf_bytes = saved_ext_bytes;
         c->stream = caller;
         return st;
     }
     if (gi_per_frame && (flags & RV_F_PREPASS) && c->pipe && c->megakernel && frames > 0) {
         hipStream_t S = own0 ? c->fstreams[0] : caller;
-        st = render_gi_pipe(c, frames, cam, vp16, pvp16, time, jx, jy, flags, S, comm);
+        st = render_gi_pipe(c, q, flags, S, comm);
         c->stream = caller;
         if (st != RV_OK) return st;
         if (S != caller) HIP_TRY(c, hipStreamWaitEvent(caller, c->slots[0].done, 0));
@@ -1880,7 +2029,7 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
     }
     if (gi_per_frame && (flags & RV_F_PREPASS) && !tiles && n > 1 && c->megakernel && frames > 0) {
         hipStream_t S = own0 ? c->fstreams[0] : caller;
-        st = render_gi_groups(c, frames, cam, vp16, pvp16, time, jx, jy, flags, S);
+        st = render_gi_groups(c, q, flags, S);
         c->stream = caller;
         if (st != RV_OK) return st;
         if (S != caller) HIP_TRY(c, hipStreamWaitEvent(caller, c->slots[0].done, 0));
@@ -1892,10 +2041,12 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
         const int si = gi_per_frame ? 0 : s;
         c->stream = own0 ? c->fstreams[si] : (si == 0 ? caller : c->fstreams[si - 1]);
         if (gi_per_frame && (st = rv_update_gi_data(c)) != RV_OK) break;
-        if (!tiles) { st = rv_frame(c, cam, vp16, pvp16, time, jx, jy, flags); continue; }
+        const rv_frame_desc& d = q.at(k);
+        if (!tiles) { st = rv_frame(c, &d.cam, d.vp, d.prev_vp, d.time, d.jitter_x, d.jitter_y, flags); continue; }
         FrameSlot& sl = c->slots[s];
         c->ext_tilebuf = sl.tbuf; c->ext_tilebuf_bytes = sl.tbytes;
-        st = rv_frame_tiles(c, cam, vp16, pvp16, time, jx, jy, flags, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T);
+        st = rv_frame_tiles(c, &d.cam, d.vp, d.prev_vp, d.time, d.jitter_x, d.jitter_y, flags, c->shard_ids.data(),
+                            (int32_t)c->shard_ids.size(), T);
         if (st != RV_OK) break;
         HIP_TRY(c, hipEventRecord(sl.done, c->stream));   // the render, also with one slot
         sl.pending = true;
@@ -1933,6 +2084,37 @@ rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, cons
         HIP_TRY(c, hipStreamWaitEvent(caller, c->ev_loop, 0));
     }
     return RV_OK;
+}
+
+rv_status rv_render_frame_seq(rv_ctx* c, int32_t frames, const rv_frame_desc* seq, const rv_frame_desc* next,
+                              int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
+    if (!c || frames < 0 || (frames > 0 && !seq)) return RV_ERR_INVALID;
+    if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_render_frame_seq before world");
+    if (comm && (c->shard_n != comm->nranks || c->shard_rank != comm->rank))
+        return fail(c, RV_ERR_INVALID, "tile shard does not match the communicator");
+    if (frames == 0) return RV_OK;
+    Seq q;
+    q.d = seq; q.stride = 1; q.n = frames; q.next = next;
+    return render_seq(c, q, flags, gi_per_frame, comm);
+}
+
+rv_status rv_render_frames(rv_ctx* c, int32_t frames, const rv_camera* cam, const float* vp16, const float* pvp16,
+                           float time, float jx, float jy, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
+    if (!c || !cam || frames < 0) return RV_ERR_INVALID;
+    if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_render_frames before world");
+    if (comm && (c->shard_n != comm->nranks || c->shard_rank != comm->rank))
+        return fail(c, RV_ERR_INVALID, "tile shard does not match the communicator");
+    if (frames == 0) return RV_OK;
+    rv_frame_desc d;
+    d.cam = *cam;
+    for (int i = 0; i < 16; i++) {
+        d.vp[i] = vp16 ? vp16[i] : (i % 5 == 0 ? 1.0f : 0.0f);
+        d.prev_vp[i] = pvp16 ? pvp16[i] : d.vp[i];
+    }
+    d.time = time; d.jitter_x = jx; d.jitter_y = jy;
+    Seq q;
+    q.d = &d; q.stride = 0; q.n = frames;
+    return render_seq(c, q, flags, gi_per_frame, comm);
 }
 
 }  // extern "C"

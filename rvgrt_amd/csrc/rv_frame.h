@@ -44,8 +44,19 @@ __device__ __forceinline__ uint32_t batch_block(const FrameParams& f, uint32_t& 
     return b;
 }
 
-// Frame b of a batched launch: its outputs (wave-uniform, SGPR math).
+// Frame b of a batched launch: its camera (per-frame table) and its outputs
+// (wave-uniform, SGPR math).
+// CAMS: the launch has a per-frame camera table (instantiated separately:
+// the table's loads cost the kernels without one 3 VGPRs).
+template <bool CAMS = false>
 __device__ __forceinline__ void batch_frame(FrameParams& f, uint64_t b) {
+    f.cam = nullptr;
+    if (CAMS) {
+        const FrameCam* c = f.cams + b;
+        f.cam = c;
+        f.pos = c->pos; f.fo = c->fo; f.ri = c->ri; f.up = c->up;
+        f.time = c->time; f.jx = c->jx; f.jy = c->jy;
+    }
     if (b == 0) return;
     f.color = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(f.color) + b * f.bs_color);
     if (f.mv) f.mv = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(f.mv) + b * f.bs_mv);

@@ -38,6 +38,14 @@ constexpr size_t QCOUNT_BYTES = (size_t)NQUEUE * NXCD * QC_STRIDE * 4;
 // hinfo bits of a primary hit record
 enum : uint32_t { HI_HIT = 1u, HI_UNDEF = 2u, HI_WATER = 4u, HI_SHADOWED = 8u, HI_NSHIFT = 4 };
 
+// One frame's camera (rv_frame_desc): the table a batched launch reads when
+// its frames have different cameras (FrameParams::cams).
+struct FrameCam {
+    f3 pos, fo, ri, up;
+    float time, jx, jy;
+    float vp[16], pvp[16];
+};
+
 struct FrameParams {
     int sched;
     const int* chunk_order[2];   // SCHED_COST: chunks by descending cost of the last frame (CG_*)
@@ -67,6 +75,8 @@ struct FrameParams {
     // frame batch (rv_render_frames): frame blockIdx.y of the launch writes
     // images, half-res images and packed tiles this many bytes further on
     uint64_t bs_color, bs_mv, bs_depth, bs_half, bs_tile;
+    const FrameCam* cams;   // batched launch with per-frame cameras: frame b's camera is cams[b] (else the fields above)
+    const FrameCam* cam;    // set on the device by batch_frame: this frame's entry of cams (nullptr: the fields above)
     uint32_t nbatch;        // frames in the launch
     uint32_t ileave;        // > 1: frames interleaved along grid x (batch_block), else grid y = frame
 };
@@ -88,6 +98,7 @@ struct PipeParams {
     uint32_t gi_frame;
     uint32_t part[3], len[3];
     float* pp_hdist; float* pp_hshadow;
+    f3 pp_pos, pp_fo, pp_ri, pp_up; float pp_jx, pp_jy;   // camera of the pre-pass part (frame k+1)
     unsigned long long* pp_counters;
     unsigned long long* gi_counters;
     uint32_t* wave_max;     // diagnostics (env RV_PIPE_WAVE_STATS): per workgroup, part << 30 | 10-ns ticks

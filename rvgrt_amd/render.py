@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import RvError, rv_camera, rv_config, rv_hit, rv_stats
+from ._lib import RvError, rv_camera, rv_config, rv_frame_desc, rv_hit, rv_stats
 
 
 def _ptr(a: np.ndarray):
@@ -31,6 +31,20 @@ def camera_from_pose(pos, yaw, pitch, width, height):
     if st != 0:
         raise RvError(f"rv_camera_from_pose: {_lib.STATUS_NAMES.get(st, st)}")
     return cam, vp
+
+
+def frame_desc(cam: rv_camera, vp, prev_vp=None, time=0.0, jx=0.0, jy=0.0) -> rv_frame_desc:
+    """One frame's inputs (rv_frame_desc): camera, unjittered VP and the
+    previous frame's, effective time and jitter."""
+    d = rv_frame_desc()
+    d.cam = cam
+    vp = np.ascontiguousarray(vp, np.float32)
+    pvp = vp if prev_vp is None else np.ascontiguousarray(prev_vp, np.float32)
+    for i in range(16):
+        d.vp[i] = float(vp[i])
+        d.prev_vp[i] = float(pvp[i])
+    d.time, d.jitter_x, d.jitter_y = float(time), float(jx), float(jy)
+    return d
 
 
 def camera_dict(cam: rv_camera, vp):
@@ -236,6 +250,16 @@ class StateRender:
         self._check(self._L.rv_render_frames(self._h, int(n), C.byref(cam), _ptr(vp), _ptr(pvp), float(time),
                                              float(jx), float(jy), f, int(bool(gi_per_frame)),
                                              comm._h if comm is not None else None), "rv_render_frames")
+
+    def render_frame_seq(self, descs, next_desc=None, flags=None, gi_per_frame=False, comm=None):
+        """rv_render_frame_seq: one rv_frame_desc per frame (moving camera,
+        jitter/time sequence); next_desc = the frame after the sequence."""
+        n = len(descs)
+        arr = (rv_frame_desc * max(n, 1))(*descs)
+        f = self.flags if flags is None else int(flags)
+        nxt = C.byref(next_desc) if next_desc is not None else None
+        self._check(self._L.rv_render_frame_seq(self._h, n, arr, nxt, f, int(bool(gi_per_frame)),
+                                                comm._h if comm is not None else None), "rv_render_frame_seq")
 
     def tile_buffer(self):
         p, n = C.c_void_p(), C.c_size_t()

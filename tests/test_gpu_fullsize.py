@@ -101,10 +101,11 @@ def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=6):
     dep = r.readback(rv.RV_IMAGE_DEPTH)
     fr = oracle.make_frame(W, H, flags, cam_d, time=time)
     rows = sorted(set(rng.integers(0, H, nrows).tolist()) | {0, H // 2, H - 1})
-    for y in rows:
-        ref = oracle.render(ow, fr, y, y + 1, want_stats=False)
-        assert np.array_equal(img[y], ref["rgba"][y]), f"row {y}"
-        assert np.array_equal(mv[y], ref["mv"][y]) and np.array_equal(dep[y], ref["depth"][y]), f"row {y}"
+    ref = oracle.render_rows(ow, fr, rows, want_stats=False)
+    d = np.abs(img[rows].astype(np.int32) - ref["rgba"][rows].astype(np.int32)).max(axis=-1)
+    print(f"rows {rows}: {int((d > 0).sum())} of {d.size} pixels differ, max |d| {int(d.max())}")
+    assert d.max() <= 2 and (d == 0).mean() >= 0.995                       # the frame tolerance (powf ulps)
+    assert np.array_equal(mv[rows], ref["mv"][rows]) and np.array_equal(dep[rows], ref["depth"][rows])
     return rows
 
 
@@ -180,8 +181,8 @@ def test_reference_native_config_draw_cuda(rv, atlas, oracle):
     # how much the R6 fetch matters on this frame: the same rows with exact texel indices (informational)
     fr = oracle.make_frame(W, H, flags, d, time=0.7)
     img = r.readback(rv.RV_IMAGE_COLOR)
-    ndiff = sum(int(np.any(oracle.render(ow, fr, y, y + 1, want_stats=False)["rgba"][y] != img[y], axis=-1).sum())
-                for y in rows)
+    plain = oracle.render_rows(ow, fr, rows, want_stats=False)["rgba"][rows]
+    ndiff = int(np.any(plain != img[rows], axis=-1).sum())
     print(f"native frame: {ndiff} pixels of {len(rows)} rows differ between the reference fetch and exact texels")
     r.close()
 

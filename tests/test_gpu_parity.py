@@ -488,7 +488,8 @@ def test_pipelined_frames_stats(rv, atlas):
     r.render_frames(3, cam, vp, flags=flags, gi_per_frame=True)
     three = {k: r.stats(k) for k in range(8)}
     assert three[2]["traces"] == 3 * one[2]["traces"]          # render: 3 frames
-    assert three[0]["traces"] == 3 * one[0]["traces"]          # pre-pass: frame 0 + two pipelined
+    # pre-pass: frame 0, frames 1 and 2 pipelined, and frame 3's, kept for the next call
+    assert three[0]["traces"] == 4 * one[0]["traces"]
     assert three[7]["gi_traces"] > 0
     r.close()
 
@@ -515,5 +516,89 @@ def test_render_frames_two_streams(rv, atlas, monkeypatch):
     r.render_frames(13, cam, vp, comm=comm)
     assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), want)
     comm.close()
+    r.close()
+    ref.close()
+
+
+def _frame_one(ref, rv, d, flags, gi):
+    """One frame of a sequence the reference's way: UpdateGIData, then the frame."""
+    if gi:
+        ref.update_gi_data()
+    ref.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time, jx=d.jitter_x,
+              jy=d.jitter_y, flags=flags)
+
+
+def _images(r, rv):
+    return [r.readback(k).copy() for k in (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH)]
+
+
+@pytest.mark.parametrize("jitter", ["ref_compat", "rays"])
+def test_frame_seq_pipelined_moving_camera(rv, atlas, oracle, jitter):
+    """rv_render_frame_seq on the pipelined reference loop with a moving
+    camera (yaw pan, the jitter sequence as time or as ray jitter, previous
+    VP = the previous frame's): frames, motion vectors and the GI grid equal
+    one-at-a-time frames after every call.  The next frame's update and
+    pre-pass kept between calls are used when the next call starts where the
+    last ended, dropped when it does not (a different camera) or when a GI
+    write came in between."""
+    from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    lg, W, H, rays = 7, 320, 192, 5000
+    flags = rv.RV_FLAGS_REFERENCE
+    seq = camera_path(TEST_POSES_128["P0"], W, H, 14, pan=0.02, ref_compat=jitter == "ref_compat")
+
+    def make():
+        r = rv.StateRender((lg,) * 3, W, H, flags=flags, atlas=atlas, gi_rays_per_frame=rays)
+        r.world_build()
+        r.gi_update(0)
+        return r
+    ref, r = make(), make()
+    ref.set_pipeline(0)
+    # (first, end, next index): kept work used (calls 1, 2), pre-pass kept for seq[8] but the next call
+    # starts at seq[9] (call 3: update used, pre-pass recomputed), a GI write before call 4 (update
+    # recomputed, pre-pass used)
+    calls = [(0, 3, 3), (3, 7, 7), (7, 9, None), (9, 11, 11), (11, 14, None)]
+    for i, (a, b, nxt) in enumerate(calls):
+        if i == 4:   # a GI write between calls: the kept update is stale
+            r.gi_update(9, first=100, count=300)
+            ref.gi_update(9, first=100, count=300)
+        r.render_frame_seq(seq[a:b], next_desc=seq[nxt] if nxt is not None else None, gi_per_frame=True)
+        for k in range(a, b):
+            _frame_one(ref, rv, seq[k], flags, True)
+        for x, y in zip(_images(r, rv), _images(ref, rv)):
+            assert np.array_equal(x, y), (a, b)
+        assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ref.world_export(rv.RV_WORLD_GI)), (a, b)
+    assert np.abs(r.readback(rv.RV_IMAGE_MOTION).view(np.float16).astype(np.float32)).max() > 0   # camera moved
+    r.close()
+    ref.close()
+
+
+@pytest.mark.parametrize("flags", [0, 8])
+def test_frame_seq_batched_moving_camera(rv, atlas, flags):
+    """Batched groups (no per-frame GI update) with a camera per frame: the
+    group launch reads each frame's camera from the device table; the last
+    frame of sequences of several lengths (whole groups, a partial group,
+    equal split groups) equals that frame rendered alone -- whole frames, a
+    one-rank tile shard and the one-rank RCCL gather path."""
+    from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    lg, W, H = 7, 320, 192
+    seq = camera_path(TEST_POSES_128["P1"], W, H, 21, pan=0.03, ref_compat=False)
+    ref = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=flags, gi_sweeps=1)
+    r.set_frames_in_flight(4)
+    for shard in ("none", "one_rank", "rccl"):
+        comm = None
+        if shard == "one_rank":
+            r.set_tile_shard(16, 0, 1)
+        elif shard == "rccl":
+            comm = rv.Comm(r, rv.Comm.unique_id(), 1, 0)
+        for n in (4, 7, 21):
+            r.render_frame_seq(seq[:n], flags=flags, comm=comm)
+            _frame_one(ref, rv, seq[n - 1], flags, False)
+            assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref.readback(rv.RV_IMAGE_COLOR)), (shard, n)
+            if shard == "none":
+                assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref.readback(rv.RV_IMAGE_MOTION)), n
+                assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref.readback(rv.RV_IMAGE_DEPTH)), n
+        if comm is not None:
+            comm.close()
     r.close()
     ref.close()

@@ -18,7 +18,7 @@ run() {  # name limit cmd...
 for step in "$@"; do
     case $step in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
-        tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ${TESTS_K:+-k "$TESTS_K"}
+        tests) run tests 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider ${TESTS_K:+-k "$TESTS_K"}
                rc=$?; [ $rc -le 1 ] || exit 3 ;;
         bench) run bench 600 python bench.py || exit 3 ;;
         bench_c3) run bench_c3 600 python bench.py --config c3 --cpu-seconds 5 || exit 3 ;;
