@@ -10,9 +10,9 @@ from ._lib import (RV_F_GI, RV_F_PREPASS, RV_F_REF_FETCH, RV_F_SHADOW, RV_F_STAT
                    RV_IMAGE_HALF_SHADOW, RV_IMAGE_MOTION, RV_WORLD_BITS, RV_WORLD_CSDF,
                    RV_WORLD_GI, RvError)
 from .configs import CONFIGS, RenderConfig
-from .render import Comm, StateRender, camera_dict, camera_from_pose, frame_desc
+from .render import Comm, LoopbackGroup, StateRender, camera_dict, camera_from_pose, frame_desc
 
-__all__ = ["StateRender", "Comm", "camera_from_pose", "camera_dict", "frame_desc", "CONFIGS", "RenderConfig", "RvError",
+__all__ = ["StateRender", "Comm", "LoopbackGroup", "camera_from_pose", "camera_dict", "frame_desc", "CONFIGS", "RenderConfig", "RvError",
            "RV_F_GI", "RV_F_PREPASS", "RV_F_REF_FETCH", "RV_F_SHADOW", "RV_F_STATS", "RV_F_WATER",
            "RV_FLAGS_REFERENCE", "RV_IMAGE_COLOR", "RV_IMAGE_DEPTH", "RV_IMAGE_HALF_DIST",
            "RV_IMAGE_HALF_SHADOW", "RV_IMAGE_MOTION", "RV_WORLD_BITS", "RV_WORLD_CSDF",

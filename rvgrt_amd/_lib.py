@@ -108,6 +108,12 @@ SIGNATURES = [
     ("rv_comm_unique_id", I32, [C.c_char_p, P, SZ]),
     ("rv_comm_create", I32, [P, C.c_char_p, P, SZ, I32, I32, C.POINTER(P)]),
     ("rv_comm_destroy", None, [P]),
+    ("rv_comm_wait", I32, [P, I32]),
+    ("rv_loopback_group_create", I32, [I32, I32, C.POINTER(P)]),
+    ("rv_loopback_group_destroy", None, [P]),
+    ("rv_comm_create_loopback", I32, [P, P, I32, I32, C.POINTER(P)]),
+    ("rv_set_tile_shard_weighted", I32, [P, I32, I32, I32, F]),
+    ("rv_set_gather_bpp", I32, [P, I32]),
     ("rv_set_tile_shard", I32, [P, I32, I32, I32]),
     ("rv_render_frames", I32, [P, I32, C.POINTER(rv_camera), P, P, F, F, F, I32, I32, P]),
     ("rv_render_frame_seq", I32, [P, I32, C.POINTER(rv_frame_desc), C.POINTER(rv_frame_desc), I32, I32, P]),

@@ -7,6 +7,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <tuple>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +21,10 @@
 #include "rv_frame.h"
 
 using namespace rv;
+
+static rv_status comm_wait_bounded(rv_ctx* c, rv_comm* m, double timeout_s);
+static double comm_timeout_s();
+static void comm_detach(rv_comm* m);
 
 // Device copy of a host id list, uploaded only when the list changes.
 struct DevIds {
@@ -154,6 +162,8 @@ struct rv_ctx {
     uint64_t carry_chunk = 0; int carry_n = 0, carry_r = 0, carry_half = 0;
     float carry_key[24] = {};
     int pipe_carry = 1;            // RV_PIPE_CARRY
+    rv_comm* comm_attached = nullptr;   // the communicator of the last rv_render_frame_seq (bounded rv_sync)
+    float shard_w0 = 1.0f;              // rank 0's tile weight of the shard (rv_set_tile_shard_weighted)
     // per-frame camera table of batched launches (rv_render_frame_seq): device copy, pinned staging
     FrameCam* cam_dev = nullptr; FrameCam* cam_host = nullptr; size_t cam_cap = 0;
     hipEvent_t cam_ev = nullptr; bool cam_pending = false;
@@ -350,7 +360,10 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
-    if (const char* e = getenv("RV_GATHER_BPP")) c->gather_bpp = atoi(e) == 4 ? 4 : 3;
+    if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
+        if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
+        c->gather_bpp = atoi(e);
+    }
     if (const char* e = getenv("RV_PIPE_ORDER")) {   // a permutation of the parts, else the default
         const uint32_t o = (uint32_t)strtoul(e, nullptr, 16);
         const uint32_t a = o >> 8 & 0xF, b = o >> 4 & 0xF, d = o & 0xF;
@@ -389,7 +402,12 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
 void rv_destroy(rv_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
-    hipDeviceSynchronize();   // every frame slot's stream
+    if (c->comm_attached) {   // a communicator still open: never hang on a dead peer
+        if (comm_wait_bounded(c, c->comm_attached, comm_timeout_s()) == RV_OK) hipDeviceSynchronize();
+        comm_detach(c->comm_attached);
+    } else {
+        hipDeviceSynchronize();   // every frame slot's stream
+    }
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
     for (auto& ph : c->pipe_half) { hipFree(ph[0]); hipFree(ph[1]); }
     for (int q = 0; q < 2; q++) { hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]); }
@@ -581,6 +599,7 @@ rv_status rv_set_gi_stats(rv_ctx* c, int32_t on) {
 
 rv_status rv_sync(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
+    if (c->comm_attached) return comm_wait_bounded(c, c->comm_attached, comm_timeout_s());   // never hangs on a peer
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->slots.size() > 1)
         for (const FrameSlot& sl : c->slots)
@@ -1314,6 +1333,8 @@ struct RcclApi {
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
+    ncclResult_t (*async_error)(ncclComm_t, ncclResult_t*) = nullptr;   // optional
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;                   // optional
 };
 RcclApi g_rccl;
 
@@ -1336,6 +1357,8 @@ bool rccl_load(const char* path, std::string& err) {
     g_rccl.group_start = (decltype(g_rccl.group_start))sym("ncclGroupStart");
     g_rccl.group_end = (decltype(g_rccl.group_end))sym("ncclGroupEnd");
     g_rccl.error_string = (decltype(g_rccl.error_string))sym("ncclGetErrorString");
+    g_rccl.async_error = (decltype(g_rccl.async_error))sym("ncclCommGetAsyncError");
+    g_rccl.comm_abort = (decltype(g_rccl.comm_abort))sym("ncclCommAbort");
     if (!g_rccl.get_unique_id || !g_rccl.comm_init_rank || !g_rccl.comm_destroy || !g_rccl.send || !g_rccl.recv ||
         !g_rccl.all_gather || !g_rccl.group_start || !g_rccl.group_end || !g_rccl.error_string) {
         err = "librccl lacks a required symbol";
@@ -1346,10 +1369,82 @@ bool rccl_load(const char* path, std::string& err) {
 }
 }  // namespace
 
-struct rv_comm {
-    ncclComm_t comm = nullptr;
-    int rank = 0, nranks = 1, device = 0;
+static double comm_timeout_s() {
+    if (const char* e = getenv("RV_COMM_TIMEOUT_S")) {
+        char* end = nullptr;
+        const double v = strtod(e, &end);
+        if (end && *end == '\0' && v > 0) return v;
+    }
+    return 120.0;
+}
+
+// ---------------------------------------------------------------- transport
+// Everything the loops exchange goes through four operations on a
+// communicator: an all-gather (the GI update's cells) and grouped
+// send/recv (packed tiles to rank 0).  Two backends:
+//   RCCL     -- one process per GPU over xGMI (ncclAllGather / ncclSend /
+//               ncclRecv inside ncclGroupStart/End);
+//   loopback -- N contexts of one process (one GPU): each rank's host thread
+//               posts its side of an operation, the group meets at a host
+//               barrier, and every rank enqueues on its own stream the
+//               device-to-device copies that fetch what it receives, after
+//               the senders' ready events; a second barrier lets every rank
+//               wait for the copies that read its buffers.  It runs the real
+//               multi-rank code paths (shard slices, padded deals, RGB24
+//               packing, GI all-gather) without N GPUs.
+// Waits are bounded (rv_comm_wait): a dead or diverged peer is an error
+// after a timeout, the communicator is aborted.
+struct LoopGroup {
+    struct Post {
+        int kind = 0;                   // 1 all-gather, 2 grouped send/recv
+        const void* send = nullptr; void* recv = nullptr; size_t bytes = 0;
+        std::vector<std::tuple<int, int, const void*, void*, size_t>> p2p;   // (is_send, peer, sbuf, rbuf, bytes)
+        hipEvent_t ready = nullptr, done = nullptr;
+    };
+    int n = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    uint64_t gen = 0;                   // barrier generation
+    int arrived = 0;
+    bool aborted = false;
+    std::vector<Post> post;
+    double timeout_s = 60.0;
+    // the barrier all ranks of a round pass twice; false on timeout or abort
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (aborted) return false;
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::duration<double>(timeout_s),
+                                    [&] { return gen != g || aborted; });
+        if (!ok || aborted) { aborted = true; cv.notify_all(); return false; }
+        return true;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
 };
+
+struct rv_comm {
+    ncclComm_t comm = nullptr;   // RCCL backend
+    LoopGroup* loop = nullptr;   // loopback backend (not owned)
+    int rank = 0, nranks = 1, device = 0;
+    rv_ctx* ctx = nullptr;       // the context it was created with (bounded waits, rv_comm_destroy)
+    bool in_group = false;
+    LoopGroup::Post pending;     // loopback: the ops of the open group
+    hipEvent_t ready = nullptr, done = nullptr;
+    uint64_t verified = 0;       // config record the ranks last agreed on (shard / bpp)
+    bool aborted = false;
+};
+
+static void comm_detach(rv_comm* m) { m->ctx = nullptr; }   // its context is being destroyed
 
 #define NCCL_TRY(ctx, expr)                                                                  \
     do {                                                                                     \
@@ -1357,6 +1452,141 @@ struct rv_comm {
         if (r_ != ncclSuccess)                                                               \
             return fail((ctx), RV_ERR_HIP, std::string(#expr) + ": " + g_rccl.error_string(r_)); \
     } while (0)
+
+static rv_status loop_round(rv_ctx* c, rv_comm* m, hipStream_t s);
+
+// Waits (host) until every stream of the context has drained, polling the
+// communicator's asynchronous error; on an error or after timeout_s the
+// communicator is aborted and RV_ERR_HIP returned (per-GPU
+// timeouts in the multi-GPU driver) -- a dead peer never hangs the caller.
+static rv_status comm_wait_bounded(rv_ctx* c, rv_comm* m, double timeout_s) {
+    std::vector<hipStream_t> ss = {c->stream, c->comm_stream, c->gi_stream};
+    for (hipStream_t f : c->fstreams) ss.push_back(f);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool busy = false;
+        for (hipStream_t s : ss) {
+            if (!s && s != c->stream) continue;   // an unused side stream (the caller's may be the NULL stream)
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipErrorNotReady) { busy = true; continue; }
+            if (e != hipSuccess) return fail(c, RV_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+        }
+        if (!busy) return RV_OK;
+        if (m && m->comm && g_rccl.async_error) {
+            ncclResult_t ae = ncclSuccess;
+            if (g_rccl.async_error(m->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                m->aborted = true;
+                if (g_rccl.comm_abort) g_rccl.comm_abort(m->comm);
+                return fail(c, RV_ERR_HIP, std::string("RCCL asynchronous error: ") + g_rccl.error_string(ae));
+            }
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+            if (m) {
+                m->aborted = true;
+                if (m->comm && g_rccl.comm_abort) g_rccl.comm_abort(m->comm);
+                if (m->loop) m->loop->abort();
+            }
+            return fail(c, RV_ERR_HIP, "timed out waiting for the frame loop (a peer rank stalled or died)");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+static rv_status comm_all_gather(rv_ctx* c, rv_comm* m, const void* send, void* recv, size_t bytes, hipStream_t s) {
+    if (m->aborted) return fail(c, RV_ERR_HIP, "communicator aborted");
+    if (m->comm) {
+        NCCL_TRY(c, g_rccl.all_gather(send, recv, bytes, ncclUint8, m->comm, s));
+        return RV_OK;
+    }
+    m->pending = LoopGroup::Post{};
+    m->pending.kind = 1; m->pending.send = send; m->pending.recv = recv; m->pending.bytes = bytes;
+    return loop_round(c, m, s);
+}
+
+static rv_status comm_group_start(rv_ctx* c, rv_comm* m) {
+    if (m->aborted) return fail(c, RV_ERR_HIP, "communicator aborted");
+    if (m->comm) NCCL_TRY(c, g_rccl.group_start());
+    m->in_group = true;
+    m->pending = LoopGroup::Post{};
+    m->pending.kind = 2;
+    return RV_OK;
+}
+
+static rv_status comm_send(rv_ctx* c, rv_comm* m, const void* buf, size_t bytes, int peer, hipStream_t s) {
+    if (m->comm) { NCCL_TRY(c, g_rccl.send(buf, bytes, ncclUint8, peer, m->comm, s)); return RV_OK; }
+    m->pending.p2p.emplace_back(1, peer, buf, nullptr, bytes);
+    return RV_OK;
+}
+
+static rv_status comm_recv(rv_ctx* c, rv_comm* m, void* buf, size_t bytes, int peer, hipStream_t s) {
+    if (m->comm) { NCCL_TRY(c, g_rccl.recv(buf, bytes, ncclUint8, peer, m->comm, s)); return RV_OK; }
+    m->pending.p2p.emplace_back(0, peer, nullptr, buf, bytes);
+    return RV_OK;
+}
+
+static rv_status comm_group_end(rv_ctx* c, rv_comm* m, hipStream_t s) {
+    m->in_group = false;
+    if (m->comm) { NCCL_TRY(c, g_rccl.group_end()); return RV_OK; }
+    return loop_round(c, m, s);
+}
+
+// One loopback round (see LoopGroup): post, meet, fetch, meet, release.
+static rv_status loop_round(rv_ctx* c, rv_comm* m, hipStream_t s) {
+    LoopGroup* g = m->loop;
+    if (!m->ready) HIP_TRY(c, hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+    if (!m->done) HIP_TRY(c, hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(m->ready, s));
+    m->pending.ready = m->ready; m->pending.done = m->done;
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        g->post[(size_t)m->rank] = m->pending;
+    }
+    if (!g->barrier()) { m->aborted = true; return fail(c, RV_ERR_HIP, "loopback: a peer did not arrive (timeout)"); }
+    // snapshot of the round: a peer posts its next round only after the second barrier
+    std::vector<LoopGroup::Post> post;
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        post = g->post;
+    }
+    const LoopGroup::Post& me = post[(size_t)m->rank];
+    for (int q = 0; q < g->n; q++) {
+        const LoopGroup::Post& o = post[(size_t)q];
+        if (o.kind != me.kind) { m->aborted = true; g->abort(); return fail(c, RV_ERR_HIP, "loopback: ranks diverged"); }
+    }
+    if (me.kind == 1) {   // all-gather: fetch every rank's block
+        for (int q = 0; q < g->n; q++) {
+            const LoopGroup::Post& o = post[(size_t)q];
+            if (o.bytes != me.bytes) { m->aborted = true; g->abort(); return fail(c, RV_ERR_HIP, "loopback: all-gather sizes differ"); }
+            if (q != m->rank) HIP_TRY(c, hipStreamWaitEvent(s, o.ready, 0));
+            HIP_TRY(c, hipMemcpyAsync(static_cast<char*>(me.recv) + (size_t)q * me.bytes, o.send, me.bytes,
+                                      hipMemcpyDeviceToDevice, s));
+        }
+    } else {              // grouped p2p: every recv fetches the matching send of its peer (k-th with k-th)
+        std::vector<int> used((size_t)g->n, 0);
+        for (const auto& op : me.p2p) {
+            if (std::get<0>(op)) continue;
+            const int q = std::get<1>(op);
+            if (q < 0 || q >= g->n) { m->aborted = true; g->abort(); return fail(c, RV_ERR_HIP, "loopback: bad peer"); }
+            const LoopGroup::Post& o = post[(size_t)q];
+            int seen = 0;
+            const std::tuple<int, int, const void*, void*, size_t>* match = nullptr;
+            for (const auto& so : o.p2p)
+                if (std::get<0>(so) && std::get<1>(so) == m->rank && seen++ == used[(size_t)q]) { match = &so; break; }
+            if (!match || std::get<4>(*match) != std::get<4>(op)) {
+                m->aborted = true; g->abort();
+                return fail(c, RV_ERR_HIP, "loopback: send/recv mismatch");
+            }
+            used[(size_t)q]++;
+            if (q != m->rank) HIP_TRY(c, hipStreamWaitEvent(s, o.ready, 0));
+            HIP_TRY(c, hipMemcpyAsync(std::get<3>(op), std::get<2>(*match), std::get<4>(op), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    HIP_TRY(c, hipEventRecord(m->done, s));
+    if (!g->barrier()) { m->aborted = true; return fail(c, RV_ERR_HIP, "loopback: a peer did not arrive (timeout)"); }
+    for (int q = 0; q < g->n; q++)   // my buffers are reusable once every reader's copies ran
+        if (q != m->rank) HIP_TRY(c, hipStreamWaitEvent(s, post[(size_t)q].done, 0));
+    return RV_OK;
+}
 
 // Buffers of a batch set for B frames (images, half-res images, packed tiles
 // of `slice` bytes per frame, rank 0's gather buffer of `gneed` bytes).
@@ -1579,8 +1809,8 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
         LAUNCH_CHECK(c);
         HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
     } else if (xchg) {   // ... or kept from the previous call: this rank's share, exchanged now
-        NCCL_TRY(c, g_rccl.all_gather(c->pipe_gi_stage, c->pipe_gi_all, chunk, ncclUint32, comm->comm,
-                                      c->comm_stream));
+        if (rv_status as = comm_all_gather(c, comm, c->pipe_gi_stage, c->pipe_gi_all, chunk * 4, c->comm_stream))
+            return as;
         HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
         HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[1], 0));
         HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->pipe_gi_all, count * 4, hipMemcpyDeviceToDevice, S));
@@ -1669,8 +1899,9 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
             HIP_TRY(c, hipEventRecord(c->pipe_ev[0], S));   // frame k rendered, shard k+1 computed
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->pipe_ev[0], 0));
             if (apply) {   // the update's cells from every rank, then the copy-back on S
-                NCCL_TRY(c, g_rccl.all_gather(c->pipe_gi_stage, c->pipe_gi_all, chunk, ncclUint32, comm->comm,
-                                              c->comm_stream));
+                if (rv_status as = comm_all_gather(c, comm, c->pipe_gi_stage, c->pipe_gi_all, chunk * 4,
+                                                   c->comm_stream))
+                    return as;
                 HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
                 HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[1], 0));
                 HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->pipe_gi_all, count * 4, hipMemcpyDeviceToDevice, S));
@@ -1679,15 +1910,16 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
             if (root)
                 HIP_TRY(c, hipMemcpyAsync(c->pipe_gbuf[k & 1], c->pipe_tbuf[k & 1], slice, hipMemcpyDeviceToDevice,
                                           c->comm_stream));
-            NCCL_TRY(c, g_rccl.group_start());
+            if (rv_status gs = comm_group_start(c, comm)) return gs;
             if (root) {
                 for (int r = 1; r < N; r++)
-                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(c->pipe_gbuf[k & 1]) + (size_t)r * slice, slice,
-                                            ncclUint8, r, comm->comm, c->comm_stream));
+                    if (rv_status rs = comm_recv(c, comm, reinterpret_cast<char*>(c->pipe_gbuf[k & 1]) + (size_t)r * slice,
+                                                 slice, r, c->comm_stream))
+                        return rs;
             } else {
-                NCCL_TRY(c, g_rccl.send(c->pipe_tbuf[k & 1], slice, ncclUint8, 0, comm->comm, c->comm_stream));
+                if (rv_status ss = comm_send(c, comm, c->pipe_tbuf[k & 1], slice, 0, c->comm_stream)) return ss;
             }
-            NCCL_TRY(c, g_rccl.group_end());
+            if (rv_status ge = comm_group_end(c, comm, c->comm_stream)) return ge;
             HIP_TRY(c, hipEventRecord(c->pipe_ev[2 + (k & 1)], c->comm_stream));
             if (root && k >= 1)   // frame k-1, whose gather overlapped this launch
                 if (rv_status us = untile(k - 1)) return us;
@@ -1829,15 +2061,14 @@ static rv_status render_batches(rv_ctx* c, const Seq& q, int32_t flags, rv_comm*
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, bs.rendered, 0));
             const size_t part = slice * (size_t)nb;   // one rank's frames of the group
             if (root) HIP_TRY(c, hipMemcpyAsync(bs.gbuf, bs.tbuf, part, hipMemcpyDeviceToDevice, c->comm_stream));
-            NCCL_TRY(c, g_rccl.group_start());
+            if (rv_status gs = comm_group_start(c, comm)) return gs;
             if (root) {
                 for (int q = 1; q < c->shard_n; q++)
-                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(bs.gbuf) + (size_t)q * part, part, ncclUint8, q,
-                                            comm->comm, c->comm_stream));
+                    if (rv_status rs = comm_recv(c, comm, reinterpret_cast<char*>(bs.gbuf) + (size_t)q * part, part, q, c->comm_stream)) return rs;
             } else {
-                NCCL_TRY(c, g_rccl.send(bs.tbuf, part, ncclUint8, 0, comm->comm, c->comm_stream));
+                if (rv_status ss = comm_send(c, comm, bs.tbuf, part, 0, c->comm_stream)) return ss;
             }
-            NCCL_TRY(c, g_rccl.group_end());
+            if (rv_status ge = comm_group_end(c, comm, c->comm_stream)) return ge;
             HIP_TRY(c, hipEventRecord(bs.gathered, c->comm_stream));
             if (root) {   // assemble the previous group now: its gather overlapped this group's render
                 if (prev_k >= 0)
@@ -1898,7 +2129,7 @@ rv_status rv_comm_create(rv_ctx* c, const char* rccl_path, const void* id, size_
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     rv_comm* m = new rv_comm();
-    m->rank = rank; m->nranks = nranks; m->device = c->device;
+    m->rank = rank; m->nranks = nranks; m->device = c->device; m->ctx = c;
     ncclResult_t r = g_rccl.comm_init_rank(&m->comm, nranks, u, rank);
     if (r != ncclSuccess) {
         delete m;
@@ -1908,13 +2139,44 @@ rv_status rv_comm_create(rv_ctx* c, const char* rccl_path, const void* id, size_
     return RV_OK;
 }
 
+rv_status rv_loopback_group_create(int32_t nranks, int32_t timeout_ms, void** out) {
+    if (nranks < 1 || !out) return RV_ERR_INVALID;
+    LoopGroup* g = new LoopGroup();
+    g->n = nranks;
+    g->post.resize((size_t)nranks);
+    if (timeout_ms > 0) g->timeout_s = timeout_ms * 1e-3;
+    *out = g;
+    return RV_OK;
+}
+
+void rv_loopback_group_destroy(void* group) { delete static_cast<LoopGroup*>(group); }
+
+rv_status rv_comm_create_loopback(rv_ctx* c, void* group, int32_t nranks, int32_t rank, rv_comm** out) {
+    LoopGroup* g = static_cast<LoopGroup*>(group);
+    if (!c || !g || !out || nranks != g->n || rank < 0 || rank >= nranks) return RV_ERR_INVALID;
+    rv_comm* m = new rv_comm();
+    m->loop = g; m->rank = rank; m->nranks = nranks; m->device = c->device; m->ctx = c;
+    *out = m;
+    return RV_OK;
+}
+
+rv_status rv_comm_wait(rv_comm* m, int32_t timeout_ms) {
+    if (!m || !m->ctx) return RV_ERR_INVALID;
+    return comm_wait_bounded(m->ctx, m, timeout_ms > 0 ? timeout_ms * 1e-3 : comm_timeout_s());
+}
+
 void rv_comm_destroy(rv_comm* m) {
     if (!m) return;
-    if (m->comm && g_rccl.comm_destroy) {
+    rv_ctx* c = m->ctx;
+    const bool ok = !c || comm_wait_bounded(c, m, comm_timeout_s()) == RV_OK;
+    if (c && c->comm_attached == m) c->comm_attached = nullptr;
+    if (m->comm) {
         hipSetDevice(m->device);
-        hipDeviceSynchronize();
-        g_rccl.comm_destroy(m->comm);
+        if (ok && !m->aborted && g_rccl.comm_destroy) g_rccl.comm_destroy(m->comm);
+        else if (g_rccl.comm_abort) g_rccl.comm_abort(m->comm);   // a peer is gone: do not wait for it
     }
+    if (m->ready) hipEventDestroy(m->ready);
+    if (m->done) hipEventDestroy(m->done);
     delete m;
 }
 
@@ -1939,18 +2201,17 @@ rv_status rv_tile_shard_assign(int32_t width, int32_t height, int32_t tile_px, i
     return RV_OK;
 }
 
-rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks) {
+rv_status rv_set_tile_shard_weighted(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks, float root_weight) {
     if (!c || nranks < 0 || (nranks > 0 && (rank < 0 || rank >= nranks))) return RV_ERR_INVALID;
     if (nranks > 0 && (tile_px < 16 || (tile_px & 15))) return fail(c, RV_ERR_INVALID, "tile_px must be a multiple of 16");
-    c->shard_n = nranks; c->shard_rank = rank; c->shard_px = tile_px;
+    if (!(root_weight > 0.0f && root_weight <= 1.0f)) return fail(c, RV_ERR_INVALID, "root weight must be in (0, 1]");
+    c->shard_n = nranks; c->shard_rank = rank; c->shard_px = tile_px; c->shard_w0 = root_weight;
     c->shard_ids.clear(); c->shard_all.clear(); c->shard_max = 0;
     if (nranks == 0) return RV_OK;
     const int tx = (c->cfg.width + tile_px - 1) / tile_px, ty = (c->cfg.height + tile_px - 1) / tile_px;
     const int nt = tx * ty;
-    double w0 = 1.0;
-    if (const char* e = getenv("RV_SHARD_ROOT_WEIGHT")) w0 = atof(e);
     std::vector<int32_t> owner((size_t)nt);
-    if (rv_status as = rv_tile_shard_assign(c->cfg.width, c->cfg.height, tile_px, nranks, (float)w0, owner.data()))
+    if (rv_status as = rv_tile_shard_assign(c->cfg.width, c->cfg.height, tile_px, nranks, root_weight, owner.data()))
         return fail(c, as, "rv_tile_shard_assign");
     std::vector<std::vector<int32_t>> own((size_t)nranks);
     for (int t = 0; t < nt; t++) own[(size_t)owner[(size_t)t]].push_back(t);
@@ -1962,8 +2223,65 @@ rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nr
     return RV_OK;
 }
 
+rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks) {
+    if (!c) return RV_ERR_INVALID;
+    float w0 = 1.0f;
+    if (const char* e = getenv("RV_SHARD_ROOT_WEIGHT")) {   // strict: a value that does not parse is an error
+        char* end = nullptr;
+        const double v = strtod(e, &end);
+        if (!end || end == e || *end != '\0') return fail(c, RV_ERR_INVALID, "RV_SHARD_ROOT_WEIGHT does not parse");
+        w0 = (float)v;
+    }
+    return rv_set_tile_shard_weighted(c, tile_px, rank, nranks, w0);
+}
+
+rv_status rv_set_gather_bpp(rv_ctx* c, int32_t bpp) {
+    if (!c || (bpp != 3 && bpp != 4)) return RV_ERR_INVALID;
+    c->gather_bpp = bpp;
+    return RV_OK;
+}
+
+// The ranks of a communicator must agree on everything that shapes the
+// exchange (shard, deal weight, packing, frame size, GI window), or the
+// slices and all-gathers would mismatch: checked with one all-gather of a
+// hash when the configuration changes (then a bounded host wait).
+static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) { for (int b = 0; b < 8; b++) { h ^= (v >> (8 * b)) & 255u; h *= 1099511628211ull; } };
+    uint32_t w0;
+    std::memcpy(&w0, &c->shard_w0, 4);
+    mix((uint64_t)comm->nranks); mix((uint64_t)c->shard_n); mix((uint64_t)c->shard_px); mix((uint64_t)c->gather_bpp);
+    mix(w0); mix((uint64_t)c->shard_max); mix((uint64_t)c->cfg.width); mix((uint64_t)c->cfg.height);
+    mix((uint64_t)c->cfg.gi_rays_per_frame); mix((uint64_t)(flags & ~RV_F_STATS));
+    for (int32_t t : c->shard_all) mix((uint64_t)(uint32_t)t);
+    if (comm->verified == h) return RV_OK;
+    if (!c->comm_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    uint64_t* d = nullptr;
+    HIP_TRY(c, hipMalloc(&d, 8 * (size_t)(comm->nranks + 1)));
+    std::vector<uint64_t> all((size_t)comm->nranks, 0);
+    rv_status st = RV_OK;
+    if (hipMemcpyAsync(d + comm->nranks, &h, 8, hipMemcpyHostToDevice, c->comm_stream) != hipSuccess)
+        st = fail(c, RV_ERR_HIP, "hipMemcpyAsync");
+    if (st == RV_OK) st = comm_all_gather(c, comm, d + comm->nranks, d, 8, c->comm_stream);
+    if (st == RV_OK && hipMemcpyAsync(all.data(), d, 8 * all.size(), hipMemcpyDeviceToHost, c->comm_stream) != hipSuccess)
+        st = fail(c, RV_ERR_HIP, "hipMemcpyAsync");
+    if (st == RV_OK) st = comm_wait_bounded(c, comm, comm_timeout_s());
+    hipFree(d);
+    if (st != RV_OK) return st;
+    for (int r = 0; r < comm->nranks; r++)
+        if (all[(size_t)r] != h)
+            return fail(c, RV_ERR_INVALID, "ranks disagree on the shard / deal weight / gather packing / frame config "
+                                            "(rank " + std::to_string(r) + ")");
+    comm->verified = h;
+    return RV_OK;
+}
+
 static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
     const int frames = q.n;
+    if (comm) {
+        c->comm_attached = comm;
+        if (rv_status vs = verify_ranks(c, comm, flags)) return vs;
+    }
     if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_render_frames before world");
     if (comm && (c->shard_n != comm->nranks || c->shard_rank != comm->rank))
         return fail(c, RV_ERR_INVALID, "tile shard does not match the communicator");
@@ -2054,15 +2372,14 @@ static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_p
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, sl.done, 0));
             if (c->shard_rank == 0)
                 HIP_TRY(c, hipMemcpyAsync(sl.gbuf, sl.tbuf, slice, hipMemcpyDeviceToDevice, c->comm_stream));
-            NCCL_TRY(c, g_rccl.group_start());
+            if (rv_status gs = comm_group_start(c, comm)) return gs;
             if (c->shard_rank == 0) {
                 for (int q = 1; q < c->shard_n; q++)
-                    NCCL_TRY(c, g_rccl.recv(reinterpret_cast<char*>(sl.gbuf) + (size_t)q * slice, slice, ncclUint8, q,
-                                            comm->comm, c->comm_stream));
+                    if (rv_status rs = comm_recv(c, comm, reinterpret_cast<char*>(sl.gbuf) + (size_t)q * slice, slice, q, c->comm_stream)) return rs;
             } else {
-                NCCL_TRY(c, g_rccl.send(sl.tbuf, slice, ncclUint8, 0, comm->comm, c->comm_stream));
+                if (rv_status ss = comm_send(c, comm, sl.tbuf, slice, 0, c->comm_stream)) return ss;
             }
-            NCCL_TRY(c, g_rccl.group_end());
+            if (rv_status ge = comm_group_end(c, comm, c->comm_stream)) return ge;
             HIP_TRY(c, hipEventRecord(sl.gathered, c->comm_stream));
             HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.gathered, 0));   // slot reuse after the send
             if (c->shard_rank == 0)

@@ -92,9 +92,45 @@ class Comm:
         self._h = h
         self.rank, self.nranks = int(rank), int(nranks)
 
+    @classmethod
+    def loopback(cls, render: "StateRender", group: "LoopbackGroup", rank: int):
+        """Rank `rank` of an in-process loopback group (rv_comm_create_loopback)."""
+        self = cls.__new__(cls)
+        self._L = _lib.load()
+        h = C.c_void_p()
+        render._check(self._L.rv_comm_create_loopback(render._h, group._h, group.nranks, int(rank), C.byref(h)),
+                      "rv_comm_create_loopback")
+        self._h = h
+        self.rank, self.nranks = int(rank), group.nranks
+        return self
+
+    def wait(self, timeout_ms=0):
+        """rv_comm_wait: bounded wait for this rank's loop; raises on a stalled peer."""
+        st = self._L.rv_comm_wait(self._h, int(timeout_ms))
+        if st != 0:
+            raise RvError(f"rv_comm_wait: {_lib.STATUS_NAMES.get(st, st)}")
+
     def close(self):
         if getattr(self, "_h", None):
             self._L.rv_comm_destroy(self._h)
+            self._h = None
+
+
+class LoopbackGroup:
+    """N in-process ranks on one GPU (rv_loopback_group_create)."""
+
+    def __init__(self, nranks, timeout_ms=0):
+        self._L = _lib.load()
+        h = C.c_void_p()
+        st = self._L.rv_loopback_group_create(int(nranks), int(timeout_ms), C.byref(h))
+        if st != 0:
+            raise RvError(f"rv_loopback_group_create: {_lib.STATUS_NAMES.get(st, st)}")
+        self._h = h
+        self.nranks = int(nranks)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rv_loopback_group_destroy(self._h)
             self._h = None
 
 
@@ -235,9 +271,18 @@ class StateRender:
                                            float(jx), float(jy), f, _ptr(ids), len(ids),
                                            int(tile_px)), "rv_frame_tiles")
 
-    def set_tile_shard(self, tile_px, rank, nranks):
-        """This rank's interleaved share of T x T tiles for render_frames (0 ranks = full frames)."""
-        self._check(self._L.rv_set_tile_shard(self._h, int(tile_px), int(rank), int(nranks)), "rv_set_tile_shard")
+    def set_tile_shard(self, tile_px, rank, nranks, root_weight=None):
+        """This rank's interleaved share of T x T tiles for render_frames (0 ranks = full frames);
+        root_weight = rank 0's share relative to the others (default: env RV_SHARD_ROOT_WEIGHT or 1)."""
+        if root_weight is None:
+            self._check(self._L.rv_set_tile_shard(self._h, int(tile_px), int(rank), int(nranks)), "rv_set_tile_shard")
+        else:
+            self._check(self._L.rv_set_tile_shard_weighted(self._h, int(tile_px), int(rank), int(nranks),
+                                                           float(root_weight)), "rv_set_tile_shard_weighted")
+
+    def set_gather_bpp(self, bpp):
+        """Packed pixel bytes of the loop's tile gather (3 RGB24, 4 RGBA8)."""
+        self._check(self._L.rv_set_gather_bpp(self._h, int(bpp)), "rv_set_gather_bpp")
 
     def render_frames(self, n, cam, vp, prev_vp=None, time=0.0, jx=0.0, jy=0.0, flags=None,
                       gi_per_frame=False, comm=None):
