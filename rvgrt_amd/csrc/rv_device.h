@@ -26,6 +26,71 @@
 
 namespace rv {
 
+// ---------------------------------------------------------------- gather diagnostics
+// RV_GATHER_DIAG=1 builds (a variant library, never the product) record, per
+// gather site, wave-level instructions, active lanes, distinct 128-B lines over
+// the wave and distinct lines summed over its four quarter-waves -- the
+// coherence figures that price a gather on the vector L1 path
+// (profiles/r01_ubench_gather.txt).  Site = kind of trace (set by the caller
+// with RV_GD_KIND) x phase.  Counters are global 64-bit atomics from one lane
+// per instruction (slow; the figures, not the timing, are the product).
+// RV_ABLATE (timing experiments only, never the product): bits that skip a
+// part of the frame to price it -- 1 texture noise, 2 cones, 4 water
+// reflection, 8 fog, 16 MV/depth stores, 32/64/128 the GI / pre-pass / render
+// part of the pipelined launch.
+#ifndef RV_ABLATE
+#define RV_ABLATE 0
+#endif
+namespace gd {
+enum Kind { PP_PRIMARY = 0, PP_SHADOW, PRIMARY, REFL, REFL_SHADOW, SHADOW, GI_SHADOW, GI_BOUNCE, OTHER,
+            CONE, TEX, HALF, GIREAD, OUTPUT, NKIND = 16 };
+enum Phase { SPHERE = 0, DDA = 1, CHECK = 2, NPHASE = 4 };   // CONE: 0 CSDF, 1 GI texel
+enum Metric { INSTR = 0, LANES, WLINES, QLINES, NMETRIC };
+constexpr int NSLOT = NKIND * NPHASE * NMETRIC;
+}
+#if RV_GATHER_DIAG
+static __device__ unsigned long long g_gather_diag[gd::NSLOT];
+#endif
+#if RV_GATHER_DIAG && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t* gd_kind_slot() {
+    __shared__ uint32_t s_kind[16];   // one per wave of the workgroup
+    return &s_kind[threadIdx.x >> 6];
+}
+__device__ __forceinline__ uint32_t gd_distinct(uint64_t key) {
+    bool todo = true;
+    uint32_t n = 0;
+    while (true) {
+        const uint64_t m = __ballot(todo);
+        if (m == 0) break;
+        n++;
+        const int src = __builtin_ctzll(m);
+        const uint32_t lo = __shfl((uint32_t)key, src), hi = __shfl((uint32_t)(key >> 32), src);
+        if (key == (((uint64_t)hi << 32) | lo)) todo = false;
+    }
+    return n;
+}
+__device__ __forceinline__ void gd_rec(int phase, uint64_t byte_addr) {
+    const uint32_t kind = *gd_kind_slot();
+    const uint64_t act = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint64_t line = byte_addr >> 7;
+    const uint32_t nw = gd_distinct(line);
+    const uint32_t nq = gd_distinct((line << 2) | (lane >> 4));
+    if (lane == (uint32_t)__builtin_ctzll(act)) {
+        unsigned long long* s = g_gather_diag + ((kind & 15u) * gd::NPHASE + (uint32_t)phase) * gd::NMETRIC;
+        atomicAdd(s + gd::INSTR, 1ull);
+        atomicAdd(s + gd::LANES, (unsigned long long)__popcll(act));
+        atomicAdd(s + gd::WLINES, (unsigned long long)nw);
+        atomicAdd(s + gd::QLINES, (unsigned long long)nq);
+    }
+}
+#define RV_GD_KIND(k) (*::rv::gd_kind_slot() = (uint32_t)(k))
+#define RV_GD(phase, addr) ::rv::gd_rec((phase), (uint64_t)(addr))
+#else
+#define RV_GD_KIND(k) ((void)0)
+#define RV_GD(phase, addr) ((void)0)
+#endif
+
 // ---------------------------------------------------------------- vectors
 struct f3 { float x, y, z; };
 RV_HD f3 V(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -48,6 +113,18 @@ RV_HD float clampf(float v, float a, float b) { return fmaxf(a, fminf(b, v)); }
 RV_HD uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 RV_HD int imin(int a, int b) { return a < b ? a : b; }
 RV_HD int imax(int a, int b) { return a > b ? a : b; }
+
+// (float)b / 255.0f for a byte b, correctly rounded like the IEEE division it
+// replaces (~10 VALU: div_scale x2, rcp, fma x4, div_fmas, div_fixup) with one
+// multiply by the rounded reciprocal and one fma residual correction: exact for
+// every b in 0..255 (checked exhaustively, tests/test_host_trace.py).  Texels,
+// GI cells and cone samples convert 3-4 bytes each.
+RV_HD float u8f(uint32_t b) {
+    const float x = (float)b, r = 0.0039215688593685627f;   // RN(1/255)
+    const float q0 = x * r;
+    const float rem = __builtin_fmaf(-q0, 255.0f, x);
+    return __builtin_fmaf(rem, r, q0);
+}
 
 // (float)(half)x with round-to-nearest-even (cuda_fp16 __float2half_rn).
 RV_HD float hround(float x) { return (float)(_Float16)x; }
@@ -177,6 +254,11 @@ RV_HD uint32_t voxel_load(const LinearWorld& w, uint32_t off) {
 }
 RV_HD uint32_t voxel_bit(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
 RV_HD uint32_t gi_texel(const LinearWorld& w, uint64_t idx) { return w.gi[idx]; }
+// addresses of a CSDF / voxel dword (gather diagnostics only)
+RV_HD const void* csdf_ptr(const World& w, uint32_t off) { return reinterpret_cast<const char*>(w.brick) + off; }
+RV_HD const void* csdf_ptr(const LinearWorld& w, uint32_t off) { return w.csdf + off; }
+RV_HD const void* voxel_ptr(const World& w, uint32_t off) { return reinterpret_cast<const char*>(w.brick) + off; }
+RV_HD const void* voxel_ptr(const LinearWorld& w, uint32_t off) { return reinterpret_cast<const char*>(w.bits) + off; }
 
 template <class WV>
 RV_HD uint32_t csdf_at(const WV& w, int cx, int cy, int cz) {
@@ -401,6 +483,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 if (off != c_off) { c_word = csdf_load(w, off); c_off = off; }
                 d = csdf_byte(c_word, cx);
             } else {
+                RV_GD(gd::SPHERE, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
                 d = csdf_at(w, (int)cx, (int)cy, (int)cz);
             }
             if (COUNT) sc.sphere += !oob;
@@ -446,9 +529,11 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                         uint32_t cx = (uint32_t)imin(imax(jx >> 1, 0), w.SX - 1);
                         uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
                         uint32_t cz = (uint32_t)imin(imax(jz >> 1, 0), w.SZ - 1);
+                        RV_GD(gd::CHECK, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
                         cw = csdf_load(w, csdf_off(w, cx, cy, cz));
                     }
                     const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
+                    RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
                     wv[j] = voxel_load(w, voxel_word_off(w, qx, qy, qz));
                     const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
                     const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
@@ -491,6 +576,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
                 uint32_t cy = (uint32_t)imin(imax(iy >> 1, 0), w.SY - 1);
                 uint32_t cz = (uint32_t)imin(imax(iz >> 1, 0), w.SZ - 1);
+                RV_GD(gd::CHECK, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
                 jd = csdf_at(w, (int)cx, (int)cy, (int)cz);
                 if (COUNT) sc.check++;
                 st = jd > 2 ? 1 : 0;
@@ -504,6 +590,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 if (off != v_off) { v_word = voxel_load(w, off); v_off = off; }
                 word = v_word;
             } else {
+                RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
                 word = voxel_load(w, voxel_word_off(w, qx, qy, qz));
             }
             const bool solid = (word >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
@@ -573,6 +660,15 @@ RV_HD f3 trace_cone(const WV& w, f3 pos, f3 dir, uint32_t& steps) {
         if (alpha > 0.99f || cd > 64.0f) break;
         if (COUNT) steps++;
         f3 p = add(pos, scale(dir, cd));
+#if RV_GATHER_DIAG && defined(__HIP_DEVICE_COMPILE__)
+        {
+            const uint32_t gx0 = (uint32_t)imax(imin((int)(floorf(p.x) * 0.5f), w.SX - 1), 0);
+            const uint32_t gy0 = (uint32_t)imax(imin((int)(floorf(p.y) * 0.5f), w.SY - 1), 0);
+            const uint32_t gz0 = (uint32_t)imax(imin((int)(floorf(p.z) * 0.5f), w.SZ - 1), 0);
+            RV_GD_KIND(gd::CONE);
+            RV_GD(0, csdf_ptr(w, csdf_off(w, gx0, gy0, gz0)));
+        }
+#endif
         float scene = get_distance_f(w, p) * 2.0f;
         float width = cd * RV_TAN_CONE;
         if (scene < width) { alpha = 1.0f; continue; }
@@ -580,10 +676,11 @@ RV_HD f3 trace_cone(const WV& w, f3 pos, f3 dir, uint32_t& steps) {
         int gy = (int)(floorf(p.y) / 4.0f);
         int gz = (int)(floorf(p.z) / 4.0f);
         if (gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ) {
+            RV_GD(1, w.gi + ((uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx));
             uint32_t s = gi_texel(w, (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx);
-            f3 c = V((float)(s & 255u) / 255.0f, (float)((s >> 8) & 255u) / 255.0f,
-                     (float)((s >> 16) & 255u) / 255.0f);
-            float a = (float)(s >> 24) / 255.0f;
+            f3 c = V(u8f(s & 255u), u8f((s >> 8) & 255u),
+                     u8f((s >> 16) & 255u));
+            float a = u8f(s >> 24);
             float blend = (1.0f - alpha) * a;
             acc = add(acc, scale(c, blend));
             alpha += blend;
@@ -591,6 +688,99 @@ RV_HD f3 trace_cone(const WV& w, f3 pos, f3 dir, uint32_t& steps) {
         cd += fmaxf(1.5f, width * 0.5f);
     }
     return acc;
+}
+
+// The six cones of computeColor (src/StateRender.cu:110-123) with their first
+// steps' gathers issued together.  Every cone's first sample sits at cd = 3
+// (alpha 0), so its CSDF byte and GI texel addresses are known before any
+// cone runs: up to 12 loads go out at once instead of as a chain of 6 x 2
+// dependent round trips (almost every cone ends at its first step:
+// cone_steps ~= cones).  The GI texel is loaded from a clamped, always-valid
+// index and used only where the reference reads it.  Each cone then continues
+// exactly as trace_cone, and the sum keeps the reference's order.
+RV_HD f3 cone_dir(int k, f3 up, f3 right, f3 fwd) {
+    switch (k) {
+        case 0: return up;
+        case 1: return lerp(up, right, 0.5f);
+        case 2: return lerp(up, neg(right), 0.5f);
+        case 3: return lerp(up, fwd, 0.5f);
+        case 4: return lerp(up, neg(fwd), 0.5f);
+        default: return lerp(up, lerp(right, fwd, 0.5f), 0.5f);
+    }
+}
+// CB = cones per group whose first-step gathers go out together (1: each
+// cone's CSDF byte and GI texel at once, 6 round trips instead of 12; 2, 3, 6:
+// fewer round trips for more live registers).
+#ifndef RV_CONE_GROUP
+#define RV_CONE_GROUP 1
+#endif
+template <bool COUNT, int CB = RV_CONE_GROUP, class WV = World>
+RV_HD f3 trace_cones6(const WV& w, f3 pos, f3 up, f3 right, f3 fwd, uint32_t& steps) {
+    static_assert(6 % CB == 0, "cone group divides 6");
+    f3 total = V(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int k0 = 0; k0 < 6; k0 += CB) {
+        float scene0[CB];
+        uint32_t tex0[CB];
+        bool in0[CB];
+#pragma unroll
+        for (int j = 0; j < CB; j++) {
+            const f3 p = add(pos, scale(cone_dir(k0 + j, up, right, fwd), 3.0f));
+            scene0[j] = get_distance_f(w, p) * 2.0f;
+            const int gx = (int)(floorf(p.x) / 4.0f), gy = (int)(floorf(p.y) / 4.0f), gz = (int)(floorf(p.z) / 4.0f);
+            in0[j] = gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ;
+            const uint64_t gi = in0[j] ? (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx : 0;
+            tex0[j] = gi_texel(w, gi);
+        }
+#pragma unroll
+        for (int j = 0; j < CB; j++) {
+            const f3 dir = cone_dir(k0 + j, up, right, fwd);
+            f3 acc = V(0.0f, 0.0f, 0.0f);
+            float alpha = 0.0f;
+            float cd = 1.5f * 2.0f;
+            if (COUNT) steps++;
+            {   // step 0 (trace_cone's first iteration) on the preloaded values
+                const float width = cd * RV_TAN_CONE;
+                if (scene0[j] < width) {
+                    alpha = 1.0f;
+                } else {
+                    if (in0[j]) {
+                        const uint32_t s = tex0[j];
+                        f3 c = V(u8f(s & 255u), u8f((s >> 8) & 255u),
+                                 u8f((s >> 16) & 255u));
+                        float a = u8f(s >> 24);
+                        float blend = (1.0f - alpha) * a;
+                        acc = add(acc, scale(c, blend));
+                        alpha += blend;
+                    }
+                    cd += fmaxf(1.5f, width * 0.5f);
+                }
+            }
+            for (int i = 1; i < 20; ++i) {
+                if (alpha > 0.99f || cd > 64.0f) break;
+                if (COUNT) steps++;
+                f3 p = add(pos, scale(dir, cd));
+                float scene = get_distance_f(w, p) * 2.0f;
+                float width = cd * RV_TAN_CONE;
+                if (scene < width) { alpha = 1.0f; continue; }
+                int gx = (int)(floorf(p.x) / 4.0f);
+                int gy = (int)(floorf(p.y) / 4.0f);
+                int gz = (int)(floorf(p.z) / 4.0f);
+                if (gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ) {
+                    uint32_t s = gi_texel(w, (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx);
+                    f3 c = V(u8f(s & 255u), u8f((s >> 8) & 255u),
+                             u8f((s >> 16) & 255u));
+                    float a = u8f(s >> 24);
+                    float blend = (1.0f - alpha) * a;
+                    acc = add(acc, scale(c, blend));
+                    alpha += blend;
+                }
+                cd += fmaxf(1.5f, width * 0.5f);
+            }
+            total = (k0 + j) == 0 ? acc : add(total, acc);
+        }
+    }
+    return total;
 }
 
 // sampleSky (src/raytracing_functions.cu:10-26)
@@ -606,11 +796,14 @@ RV_HD f3 sample_sky(f3 dir, f3 sun) {
 template <class WV>
 RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
     const float freq = 0.05f;
-    float e = simplex3D(floorf(pos.x) * freq, floorf(pos.y) * freq, floorf(pos.z) * freq);
+    float e = 0.5f;
+    if (!(RV_ABLATE & 1)) {
+    e = simplex3D(floorf(pos.x) * freq, floorf(pos.y) * freq, floorf(pos.z) * freq);
     float e2 = simplex3D(floorf((float)((double)pos.x + 121.3)) * freq * 0.3f,
                          floorf((float)((double)pos.y + 1321.3)) * freq * 0.3f,
                          floorf((float)((double)pos.z + 721.5)) * freq * 0.3f);
     e = e * 0.4f + e2 * 0.6f;
+    }
     int tile;  // (bx,by) in 1/16 units
     if (e < -1.3f) tile = 0x10;        // stone   (0,1)
     else if (e < -1.2f) tile = 0x23;   // diamond (3,2)
@@ -627,9 +820,11 @@ RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
     float cu = uy - floorf(uy), cv = ux - floorf(ux);
     int col = imin((int)floorf(cu * (float)w.aw), w.aw - 1);
     int row = imin((int)floorf(cv * (float)w.ah), w.ah - 1);
+    RV_GD_KIND(gd::TEX);
+    RV_GD(0, w.atlas + row * w.aw + col);
     uint32_t t = w.atlas[row * w.aw + col];
-    return V((float)(t & 255u) / 255.0f, (float)((t >> 8) & 255u) / 255.0f,
-             (float)((t >> 16) & 255u) / 255.0f);
+    return V(u8f(t & 255u), u8f((t >> 8) & 255u),
+             u8f((t >> 16) & 255u));
 }
 
 }  // namespace rv

@@ -133,45 +133,87 @@ __device__ __forceinline__ void chunk_cost_report(uint32_t* cost, uint64_t t0, u
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Half-res window of an 8x8-pixel wave: the 8x8 texels of the distance and
+// shadow images from (ox, oy) = (X0/2 - 2, Y0/2 - 2), X0/Y0 the tile origin,
+// staged in LDS by one coalesced load per image (every minDist / bilinear tap
+// of the tile falls inside it when hw = W/2, hh = H/2), so the 8 taps per pixel
+// read LDS instead of 8 scattered gathers (rows of the half-res image are
+// separate 128-B lines: 8-13 lines per quarter-wave and tap).  Window texel
+// (i, j) = image[clamp(oy + j)][clamp(ox + i)], so a tap at unclamped index r
+// inside the window reads exactly what image[clamp(r)] holds; a tap outside it
+// (other resolutions) reads the image.
+struct HalfWin {
+    const float* d;   // LDS: 64 distance texels, row-major 8x8 (nullptr: no window)
+    const float* s;   // LDS: 64 shadow texels
+    int ox, oy;
+};
+// All 64 lanes of the wave call this (before any per-pixel branch): lane l
+// loads texel (l & 7, l >> 3).  lds holds 128 floats for this wave.
+__device__ __forceinline__ HalfWin half_window_load(const FrameParams& f, int X0, int Y0, float* lds) {
+    HalfWin hw;
+    hw.ox = (X0 >> 1) - 2;
+    hw.oy = (Y0 >> 1) - 2;
+    const int l = (int)(threadIdx.x & 63u);
+    const size_t q = (size_t)clampi(hw.oy + (l >> 3), 0, f.hh - 1) * f.hw + clampi(hw.ox + (l & 7), 0, f.hw - 1);
+    lds[l] = f.hdist[q];
+    lds[64 + l] = f.hshadow[q];
+    hw.d = lds;
+    hw.s = lds + 64;
+    __syncthreads();
+    return hw;
+}
+__device__ __forceinline__ float half_tap(const float* img, const float* win, const FrameParams& f, int ox, int oy,
+                                          int ru, int rv) {
+    const int wx = ru - ox, wy = rv - oy;
+    if (win && (uint32_t)wx < 8u && (uint32_t)wy < 8u) return win[wy * 8 + wx];
+    return img[(size_t)clampi(rv, 0, f.hh - 1) * f.hw + clampi(ru, 0, f.hw - 1)];
+}
+
 // minDist (StateRender.cu:182-198) with W/2 x H/2 (Appendix R6).  The
 // reference fetches with normalized coordinates: u_low = floor(x*640)/640 and
 // u_low + 1/640, each turned back into a texel by the point-sampling unit as
 // floor(u*640); RV_F_REF_FETCH restates that float path (the quad can land a
 // texel low where k/640*640 rounds below k), otherwise the texels are the
-// exact k, k+1.
-__device__ __forceinline__ float min_dist(const FrameParams& f, float x, float y) {
+// exact k, k+1.  Indices stay unclamped here; half_tap clamps (point/clamp
+// addressing, src/main.cpp:443).
+__device__ __forceinline__ float min_dist(const FrameParams& f, float x, float y, const HalfWin* hwin = nullptr) {
     int u, v, u1, v1;
     if (f.flags & RV_F_REF_FETCH) {   // wave-uniform: a scalar branch
         const float fw = (float)f.hw, fh = (float)f.hh;
         const float ul = floorf(x * fw) / fw, vl = floorf(y * fh) / fh;
         const float px = 1.0f / fw, py = 1.0f / fh;
-        u = clampi((int)floorf(ul * fw), 0, f.hw - 1);
-        u1 = clampi((int)floorf((ul + px) * fw), 0, f.hw - 1);
-        v = clampi((int)floorf(vl * fh), 0, f.hh - 1);
-        v1 = clampi((int)floorf((vl + py) * fh), 0, f.hh - 1);
+        u = (int)floorf(ul * fw);
+        u1 = (int)floorf((ul + px) * fw);
+        v = (int)floorf(vl * fh);
+        v1 = (int)floorf((vl + py) * fh);
     } else {
         u = (int)floorf(x * (float)f.hw); v = (int)floorf(y * (float)f.hh);
-        u1 = clampi(u + 1, 0, f.hw - 1); v1 = clampi(v + 1, 0, f.hh - 1);
-        u = clampi(u, 0, f.hw - 1); v = clampi(v, 0, f.hh - 1);
+        u1 = u + 1; v1 = v + 1;
     }
+    const float* win = hwin ? hwin->d : nullptr;
+    const int ox = hwin ? hwin->ox : 0, oy = hwin ? hwin->oy : 0;
     const float* hd = f.hdist;
-    float d1 = hd[(size_t)v * f.hw + u], d2 = hd[(size_t)v * f.hw + u1];
-    float d3 = hd[(size_t)v1 * f.hw + u], d4 = hd[(size_t)v1 * f.hw + u1];
+    RV_GD_KIND(gd::HALF);
+    RV_GD(0, hd + (size_t)clampi(v, 0, f.hh - 1) * f.hw + clampi(u, 0, f.hw - 1));
+    float d1 = half_tap(hd, win, f, ox, oy, u, v), d2 = half_tap(hd, win, f, ox, oy, u1, v);
+    float d3 = half_tap(hd, win, f, ox, oy, u, v1), d4 = half_tap(hd, win, f, ox, oy, u1, v1);
     return fminf(fminf(d1, d2), fminf(d3, d4));
 }
 
 // tex2D<float> linear/clamp/normalized with 1/256 weights (StateRender.cu:230)
-__device__ __forceinline__ float bilinear_tex(const FrameParams& f, float x, float y) {
+__device__ __forceinline__ float bilinear_tex(const FrameParams& f, float x, float y, const HalfWin* hwin = nullptr) {
     float xb = x * (float)f.hw - 0.5f, yb = y * (float)f.hh - 0.5f;
     float fx0 = floorf(xb), fy0 = floorf(yb);
     float a = rintf((xb - fx0) * 256.0f) / 256.0f;
     float b = rintf((yb - fy0) * 256.0f) / 256.0f;
-    int i0 = (int)fx0, j0 = (int)fy0;
-    int i1 = clampi(i0 + 1, 0, f.hw - 1), j1 = clampi(j0 + 1, 0, f.hh - 1);
-    i0 = clampi(i0, 0, f.hw - 1); j0 = clampi(j0, 0, f.hh - 1);
+    const int i0 = (int)fx0, j0 = (int)fy0, i1 = i0 + 1, j1 = j0 + 1;
+    const float* win = hwin ? hwin->s : nullptr;
+    const int ox = hwin ? hwin->ox : 0, oy = hwin ? hwin->oy : 0;
     const float* hs = f.hshadow;
-    float t00 = hs[(size_t)j0 * f.hw + i0], t10 = hs[(size_t)j0 * f.hw + i1];
-    float t01 = hs[(size_t)j1 * f.hw + i0], t11 = hs[(size_t)j1 * f.hw + i1];
+    RV_GD_KIND(gd::HALF);
+    RV_GD(1, hs + (size_t)clampi(j0, 0, f.hh - 1) * f.hw + clampi(i0, 0, f.hw - 1));
+    float t00 = half_tap(hs, win, f, ox, oy, i0, j0), t10 = half_tap(hs, win, f, ox, oy, i1, j0);
+    float t01 = half_tap(hs, win, f, ox, oy, i0, j1), t11 = half_tap(hs, win, f, ox, oy, i1, j1);
     return (1.0f - a) * (1.0f - b) * t00 + a * (1.0f - b) * t10 + (1.0f - a) * b * t01 + a * b * t11;
 }
 

@@ -60,6 +60,9 @@ struct HostHit { float pos[3], normal[3], u, v; int32_t hit, undef, sphere, dda,
 // variant: 0..3 = DDA look-ahead group 1/2/4/8, 4 = group 1 with word reuse
 int rvh_variants(void) { return 5; }
 
+// rv::u8f, the device's byte -> float conversion
+float rvh_u8f(uint32_t b) { return rv::u8f(b); }
+
 int rvh_trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
                    const float* dir, const float* dist, int64_t n, HostHit* out) {
     Hit (*fn)(const World&, f3, f3, float, StepCount&) = nullptr;

@@ -59,3 +59,15 @@ def test_host_trace_bit_exact(host_lib, oracle_world, dims, variant):
     assert np.array_equal(g["dda"], o["n_dda"])
     assert np.array_equal(g["check"], o["n_check"])
     assert g["hit"].mean() > 0.2 and (g["dda"] > 100).any()
+
+
+def test_u8f_equals_ieee_division(host_lib):
+    """rv::u8f (mul by RN(1/255) + one fma residual step), which the kernels
+    use for every RGBA8 -> float conversion, equals the correctly rounded
+    float32 division b / 255 of the reference (src/raytracing_functions.cu:59,
+    :256-262, src/CoarseArray.cu:324-351) for all 256 bytes."""
+    host_lib.rvh_u8f.restype = C.c_float
+    host_lib.rvh_u8f.argtypes = [C.c_uint32]
+    got = np.array([host_lib.rvh_u8f(b) for b in range(256)], np.float32)
+    want = np.arange(256, dtype=np.float32) / np.float32(255.0)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
