@@ -7,7 +7,7 @@ IFS=';' read -ra ITEMS <<< "$RUNS"
 for it in "${ITEMS[@]}"; do
   IFS='|' read -r name envs args <<< "$it"
   out=gpurun_out/exp_$name
-  env $envs timeout -k 10 300 python bench.py --steps 30 --warmup 5 --cpu-seconds 0 $args > $out.json 2> $out.err || exit 3
+  env $envs timeout -k 10 300 python bench.py --steps ${STEPS:-30} --warmup 5 --cpu-seconds 0 $args > $out.json 2> $out.err || exit 3
   python3 -c "
 import json; d=json.load(open('$out.json'))
 print('$name', d['ms_per_step'], {k: round(v, 4) for k, v in d['kernel_ms'].items() if v > 0.006})"
