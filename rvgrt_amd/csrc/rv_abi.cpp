@@ -162,10 +162,6 @@ struct rv_ctx {
     uint64_t carry_chunk = 0; int carry_n = 0, carry_r = 0, carry_half = 0;
     float carry_key[24] = {};
     int pipe_carry = 1;            // RV_PIPE_CARRY
-    uint32_t pipe_gi_waves = 0;    // RV_GI_WAVES: > 0 = persistent lane-refill GI part with this many waves
-    uint32_t pipe_gi_flush = 16;   // RV_GI_FLUSH: waiting lanes that trigger a batch of bounce ray starts
-    uint32_t pipe_gi_octant = 0;   // RV_GI_OCTANT: GI cells binned by bounce direction octant, octant o on XCD o
-    uint32_t* pipe_gi_rec = nullptr; uint64_t pipe_gi_rec_cells = 0;   // lane-refill GI: 24-B record per cell
     rv_comm* comm_attached = nullptr;   // the communicator of the last rv_render_frame_seq (bounded rv_sync)
     float shard_w0 = 1.0f;              // rank 0's tile weight of the shard (rv_set_tile_shard_weighted)
     // per-frame camera table of batched launches (rv_render_frame_seq): device copy, pinned staging
@@ -364,9 +360,6 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
-    if (const char* e = getenv("RV_GI_WAVES")) c->pipe_gi_waves = (uint32_t)std::max(0, atoi(e));
-    if (const char* e = getenv("RV_GI_FLUSH")) c->pipe_gi_flush = (uint32_t)std::min(64, std::max(1, atoi(e)));
-    if (const char* e = getenv("RV_GI_OCTANT")) c->pipe_gi_octant = (uint32_t)(atoi(e) != 0);
     if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
         if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
         c->gather_bpp = atoi(e);
@@ -418,7 +411,7 @@ void rv_destroy(rv_ctx* c) {
     hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
     for (auto& ph : c->pipe_half) { hipFree(ph[0]); hipFree(ph[1]); }
     for (int q = 0; q < 2; q++) { hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]); }
-    hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all); hipFree(c->pipe_gi_rec);
+    hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);
     for (hipEvent_t e : c->pipe_ev) if (e) hipEventDestroy(e);
     if (c->pipe_wstat) {   // RV_PIPE_WAVE_STATS: per part, the longest wave and the 99th percentile per launch
         const char* names[3] = {"gi", "prepass", "render"};
@@ -1874,19 +1867,7 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
         p.pp_hdist = c->pipe_half[half(k + 1)][0]; p.pp_hshadow = c->pipe_half[half(k + 1)][1];
         p.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
         p.gi_counters = cnt_gi;
-        p.gi_waves = c->pipe_gi_waves && mine ? (uint32_t)std::min<uint64_t>(c->pipe_gi_waves, (mine + 63) / 64) : 0u;
-        p.gi_flush = c->pipe_gi_flush;
-        p.gi_octant = p.gi_waves ? 0u : c->pipe_gi_octant;
-        f.gi_octant = p.gi_octant;
-        if (p.gi_waves && c->pipe_gi_rec_cells < mine) {
-            HIP_TRY(c, hipDeviceSynchronize());
-            hipFree(c->pipe_gi_rec);
-            c->pipe_gi_rec = nullptr; c->pipe_gi_rec_cells = 0;
-            HIP_TRY(c, hipMalloc(&c->pipe_gi_rec, (size_t)mine * 24));
-            c->pipe_gi_rec_cells = mine;
-        }
-        p.gi_rec = c->pipe_gi_rec;
-        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, mine, p.gi_waves) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
+        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, mine) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
                                   pipe_len(f, PIPE_RENDER, 0)};
         for (int i = 0; i < 3; i++) {
             p.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;

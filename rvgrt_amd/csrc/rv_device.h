@@ -212,19 +212,6 @@ RV_HD uint32_t voxel_load(const World& w, uint32_t off) { return load_dword(w, o
 RV_HD uint32_t voxel_bit(const World&, uint32_t x, uint32_t y) { return voxel_bit(x, y); }
 RV_HD uint32_t gi_texel(const World& w, uint64_t idx) { return w.gi[idx]; }
 
-// The brick layout read with non-temporal (streaming) loads: the lines are
-// allocated evict-first in L2 / MALL, so rays that are not re-walked (the GI
-// update's random bounces, the pre-pass's open-air marches) do not displace
-// the bricks the frame's other rays keep reusing.  Same data and results.
-struct WorldNT : World {};
-RV_HD uint32_t csdf_load(const WorldNT& w, uint32_t off) {
-    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + off));
-}
-RV_HD uint32_t voxel_load(const WorldNT& w, uint32_t off) {
-    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + off));
-}
-RV_HD WorldNT world_nt(const World& w) { WorldNT n; static_cast<World&>(n) = w; return n; }
-
 // The reference's layouts (include/cumath.cuh:33-45, include/CoarseArray.cuh:
 // 9-21): bit idx = x | y<<lx | z<<(lx+ly) in uint32 words, CSDF bytes x
 // fastest, GI RGBA8 x fastest.  Used by the reference-signature device API
@@ -658,191 +645,6 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         }
     }
     return H;
-}
-
-// ---------------------------------------------------------------- resumable trace
-// trace() as a state machine advanced one sphere step or one DDA group per
-// call (tsm_step), so a lane whose ray finished can start another ray while
-// the rest of its wave is still walking (persistent waves with lane refill,
-// see rv_kernels.hip gi_part_refill).  Same per-ray operation sequence, hit
-// record and step counts as trace<COUNT, G> (tests/test_host_trace.py checks
-// it against the oracle; tsm_trace below runs it to completion).
-enum : int { TS_SPHERE = 0, TS_DDA = 1, TS_DONE = 2 };
-struct TraceSM {
-    f3 cur, dir;
-    float ddx, ddy, ddz, tx, ty, tz;
-    int ix, iy, iz;
-    int mask, n, major, phase, status;
-};
-
-template <bool COUNT>
-RV_HD void tsm_begin(TraceSM& t, f3 cam, f3 dir, float dist_h, StepCount& sc) {
-    t.cur = add(cam, scale(dir, dist_h));
-    t.dir = dir;
-    t.ddx = dir.x != 0 ? fabsf(1.0f / dir.x) : 1e10f;
-    t.ddy = dir.y != 0 ? fabsf(1.0f / dir.y) : 1e10f;
-    t.ddz = dir.z != 0 ? fabsf(1.0f / dir.z) : 1e10f;
-    t.tx = t.ty = t.tz = 0.0f;
-    t.ix = t.iy = t.iz = 0;
-    t.mask = -128; t.n = 0; t.major = 0; t.phase = TS_SPHERE; t.status = 0;
-    if (COUNT) sc.its++;
-}
-
-template <bool COUNT, int G = RV_DDA_GROUP, class WV = World>
-RV_HD void tsm_step(const WV& w, TraceSM& t, StepCount& sc) {
-    const f3 dir = t.dir;
-    const uint32_t X = (uint32_t)w.X, Y = (uint32_t)w.Y, Z = (uint32_t)w.Z;
-    const int sx = (dir.x > 0) - (dir.x < 0), sy = (dir.y > 0) - (dir.y < 0), sz = (dir.z > 0) - (dir.z < 0);
-    if (t.phase == TS_SPHERE) {   // one approximateCSDF iteration
-        int fx = (int)floorf(t.cur.x), fy = (int)floorf(t.cur.y), fz = (int)floorf(t.cur.z);
-        const bool oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= Y) | ((uint32_t)fz >= Z);
-        const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
-        const uint32_t cy = umin((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
-        const uint32_t cz = umin((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
-        RV_GD(gd::SPHERE, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
-        const uint32_t d = csdf_at(w, (int)cx, (int)cy, (int)cz);
-        if (COUNT) sc.sphere += !oob;
-        const bool stop = oob | (d <= 1);
-        const f3 nxt = add(t.cur, scale(dir, (float)d));
-        t.cur.x = stop ? t.cur.x : nxt.x;
-        t.cur.y = stop ? t.cur.y : nxt.y;
-        t.cur.z = stop ? t.cur.z : nxt.z;
-        t.n++;
-        if (stop | (t.n == 100)) {
-            if (oob) {
-                if (COUNT) sc.its++;
-                t.status = 2; t.phase = TS_DONE;
-            } else {   // DDA set-up
-                t.ix = (int)floorf(t.cur.x); t.iy = (int)floorf(t.cur.y); t.iz = (int)floorf(t.cur.z);
-                t.tx = ((sx > 0) ? ((float)t.ix + 1.0f - t.cur.x) : (t.cur.x - (float)t.ix)) * t.ddx;
-                t.ty = ((sy > 0) ? ((float)t.iy + 1.0f - t.cur.y) : (t.cur.y - (float)t.iy)) * t.ddy;
-                t.tz = ((sz > 0) ? ((float)t.iz + 1.0f - t.cur.z) : (t.cur.z - (float)t.iz)) * t.ddz;
-                t.mask = -128; t.n = 0; t.phase = TS_DDA;
-            }
-        }
-        return;
-    }
-    if (t.phase != TS_DDA) return;
-    // one DDA group: G cells' words gathered at once, then replayed (trace's look-ahead)
-    const float ddx = t.ddx, ddy = t.ddy, ddz = t.ddz;
-    int ix = t.ix, iy = t.iy, iz = t.iz, mask = t.mask;
-    float tx = t.tx, ty = t.ty, tz = t.tz;
-    uint32_t wv[G];
-    uint32_t cw = 0;
-    const bool chk = ((t.n + G - 1) & 7) == 7;
-    {
-        int jx = ix, jy = iy, jz = iz;
-        float ux = tx, uy = ty, uz = tz;
-#pragma unroll
-        for (int j = 0; j < G; j++) {
-            if (j == G - 1 && chk) {
-                uint32_t cx = (uint32_t)imin(imax(jx >> 1, 0), w.SX - 1);
-                uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
-                uint32_t cz = (uint32_t)imin(imax(jz >> 1, 0), w.SZ - 1);
-                RV_GD(gd::CHECK, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
-                cw = csdf_load(w, csdf_off(w, cx, cy, cz));
-            }
-            const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
-            RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
-            wv[j] = voxel_load(w, voxel_word_off(w, qx, qy, qz));
-            if (G > 1) {
-                const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
-                const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
-                ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
-                jx += selx ? sx : 0; jy += sely ? sy : 0; jz += selz ? sz : 0;
-            }
-        }
-    }
-    int st = 0;
-    uint32_t jd = 0;
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-        if (COUNT) sc.its++;
-        if (j == G - 1 && chk) {
-            uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
-            jd = csdf_byte(cw, cx);
-            if (COUNT) sc.check++;
-            st = jd > 2 ? 1 : 0;
-        }
-        const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
-        const bool solid = (wv[j] >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
-        if (COUNT) sc.dda += (st == 0) & !oob;
-        st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
-        const bool go = st == 0;
-        const bool cxy = tx < ty, cxz = tx < tz, cyz = ty < tz;
-        const bool selx = go & cxy & cxz;
-        const bool sely = go & !cxy & cyz;
-        const bool selz = go & !(cxy & cxz) & !(!cxy & cyz);
-        tx = selx ? tx + ddx : tx;
-        ty = sely ? ty + ddy : ty;
-        tz = selz ? tz + ddz : tz;
-        ix += selx ? sx : 0;
-        iy += sely ? sy : 0;
-        iz += selz ? sz : 0;
-        mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
-        if (!go) break;
-    }
-    t.ix = ix; t.iy = iy; t.iz = iz; t.tx = tx; t.ty = ty; t.tz = tz; t.mask = mask;
-    t.n += G;
-    if (st == 1) {   // empty space ahead: jump and restart (the next major iteration)
-        f3 c = V((float)ix + 0.5f, (float)iy + 0.5f, (float)iz + 0.5f);
-        float tt = dot(sub(c, t.cur), dir);
-        f3 por = add(t.cur, scale(dir, tt));
-        t.cur = add(por, scale(dir, (float)jd * 2.0f));
-        t.major++;
-        if (t.major == 5) {
-            t.status = 0; t.phase = TS_DONE;
-        } else {
-            if (COUNT) sc.its++;
-            t.n = 0; t.phase = TS_SPHERE;
-        }
-    } else if (st != 0) {
-        t.status = st; t.phase = TS_DONE;
-    } else if (t.n >= 200) {   // 200 steps without a hit or a jump: miss
-        t.status = 0; t.phase = TS_DONE;
-    }
-}
-
-// The hit record of a finished TraceSM (trace's epilogue).
-RV_HD Hit tsm_hit(const TraceSM& t) {
-    Hit H;
-    H.hit = false; H.undef = false; H.its = 0;
-    H.pos = V(-500.0f, -500.0f, -500.0f);
-    H.normal = V(0.0f, 0.0f, 0.0f);
-    H.u = 0.0f; H.v = 0.0f;
-    if (t.status != 3) return H;
-    const f3 dir = t.dir;
-    const int sx = (dir.x > 0) - (dir.x < 0), sy = (dir.y > 0) - (dir.y < 0), sz = (dir.z > 0) - (dir.z < 0);
-    H.hit = true;
-    if (t.mask == 0) {
-        H.normal = V((float)-sx, 0.0f, 0.0f);
-        H.pos = add(t.cur, scale(dir, t.tx - t.ddx));
-        H.u = hround(H.pos.y - (float)t.iy);
-        H.v = hround(H.pos.z - (float)t.iz);
-        if (sx == -1) H.v = hround(1.0f - H.v);
-    } else if (t.mask == 1) {
-        H.normal = V(0.0f, (float)-sy, 0.0f);
-        H.pos = add(t.cur, scale(dir, t.ty - t.ddy));
-        H.u = hround(H.pos.x - (float)t.ix);
-        H.v = hround(H.pos.z - (float)t.iz);
-    } else if (t.mask == 2) {
-        H.normal = V(0.0f, 0.0f, (float)-sz);
-        H.pos = add(t.cur, scale(dir, t.tz - t.ddz));
-        H.u = hround(H.pos.x - (float)t.ix);
-        H.v = hround(H.pos.y - (float)t.iy);
-        if (sz == 1) H.u = hround(1.0f - H.u);
-    } else {
-        H.undef = true;   // Appendix R2: pos stays (-500)^3
-    }
-    return H;
-}
-
-template <bool COUNT, int G = RV_DDA_GROUP, class WV = World>
-RV_HD Hit tsm_trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
-    TraceSM t;
-    tsm_begin<COUNT>(t, cam, dir, dist_h, sc);
-    while (t.phase != TS_DONE) tsm_step<COUNT, G>(w, t, sc);
-    return tsm_hit(t);
 }
 
 // tanf(0.4f), correctly rounded (see oracle OR_TAN_CONE).

@@ -77,7 +77,6 @@ struct FrameParams {
     uint64_t bs_color, bs_mv, bs_depth, bs_half, bs_tile;
     const FrameCam* cams;   // batched launch with per-frame cameras: frame b's camera is cams[b] (else the fields above)
     const FrameCam* cam;    // set on the device by batch_frame: this frame's entry of cams (nullptr: the fields above)
-    uint32_t gi_octant;     // pipe_len: the GI part bins by bounce octant (PipeParams::gi_octant)
     uint32_t nbatch;        // frames in the launch
     uint32_t ileave;        // > 1: frames interleaved along grid x (batch_block), else grid y = frame
 };
@@ -103,10 +102,6 @@ struct PipeParams {
     unsigned long long* pp_counters;
     unsigned long long* gi_counters;
     uint32_t* wave_max;     // diagnostics (env RV_PIPE_WAVE_STATS): per workgroup, part << 30 | 10-ns ticks
-    uint32_t gi_waves;      // > 0: the GI part runs as this many persistent lane-refill waves (gi_part_refill)
-    uint32_t gi_flush;      // lane-refill: waiting lanes that trigger a batch of bounce ray starts
-    uint32_t* gi_rec;       // lane-refill: 6 dwords per window cell (bounce result for the shading pass)
-    uint32_t gi_octant;     // 1: GI cells binned by bounce octant, octant o on XCD o (8 workgroups per 512 cells)
 };
 
 struct RvHitDev {   // == rv_hit
@@ -130,7 +125,7 @@ uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
 // workgroups of each part of a pipelined launch; then the launch itself
-uint32_t pipe_len(const FrameParams& f, int part, uint64_t gi_count, uint32_t gi_waves = 0);
+uint32_t pipe_len(const FrameParams& f, int part, uint64_t gi_count);
 void launch_ref_pipe(hipStream_t s, const World& w, const FrameParams& f, const PipeParams& p);
 // SCHED_COST: sort n costs (order has npad >= n entries) into a descending
 // order, clearing the costs

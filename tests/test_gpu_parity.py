@@ -430,23 +430,16 @@ def test_render_frames_native_loop(rv, atlas, flags, T):
     ref.close()
 
 
-@pytest.mark.parametrize("order,gi_waves,rays,octant", [("012", 0, 5000, 0), ("210", 0, 5000, 0), ("102", 0, 5000, 0),
-                                                        ("102", 3, 5000, 0), ("102", 16, 4096, 0), ("012", 1, 4096, 0),
-                                                        ("102", 64, 2048, 0), ("102", 0, 4096, 1), ("012", 0, 5000, 1)])
-def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order, gi_waves, rays, octant):
+@pytest.mark.parametrize("order,rays", [("012", 5000), ("210", 5000), ("102", 5000), ("102", 4096), ("012", 2048)])
+def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order, rays):
     """rv_set_pipeline: render k | GI update k+1 | pre-pass k+1 in one launch.
     The frames and the GI grid equal UpdateGIData + drawCUDA one frame at a
     time, for every dispatch order of the parts, over a rolling GI window
     that wraps (5000-cell windows of a 32^3 grid: linear cell order, a partial
-    last block; 4096 / 2048: whole planes, blocked order) -- and the oracle
-    agrees on the grid (bit-exact) and the last frame.  gi_waves > 0: the GI
-    part as persistent lane-refill waves (RV_GI_WAVES; 1 wave walks the whole
-    window, 64 waves get one block or none).  octant: the GI cells binned by
-    bounce direction octant, one octant per XCD (RV_GI_OCTANT)."""
+    last block; 4096 / 2048: whole planes, blocked cell order) -- and the
+    oracle agrees on the grid (bit-exact) and the last frame."""
     from rvgrt_amd.configs import TEST_POSES_128
     monkeypatch.setenv("RV_PIPE_ORDER", order)
-    monkeypatch.setenv("RV_GI_WAVES", str(gi_waves))
-    monkeypatch.setenv("RV_GI_OCTANT", str(octant))
     lg, W, H = 7, 320, 192
     flags = rv.RV_FLAGS_REFERENCE
     cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
@@ -500,26 +493,6 @@ def test_pipelined_frames_stats(rv, atlas):
     assert three[0]["traces"] == 4 * one[0]["traces"]
     assert three[7]["gi_traces"] > 0
     r.close()
-
-
-def test_gi_refill_stats_equal(rv, atlas, monkeypatch):
-    """The lane-refill GI part (RV_GI_WAVES) does the same work as one cell per
-    lane: equal GI trace, sphere, DDA, check and texture counts per launch."""
-    from rvgrt_amd.configs import TEST_POSES_128
-    lg, W, H = 7, 160, 96
-    flags = rv.RV_FLAGS_REFERENCE | rv.RV_F_STATS
-    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
-    out = []
-    for giw, octant in (("0", "0"), ("7", "0"), ("0", "1")):
-        monkeypatch.setenv("RV_GI_WAVES", giw)
-        monkeypatch.setenv("RV_GI_OCTANT", octant)
-        r = _gpu_world(rv, atlas, lg, lg, lg, W, H)
-        r.stats_reset()
-        r.render_frames(4, cam, vp, flags=flags, gi_per_frame=True)
-        out.append(r.stats(7))
-        r.close()
-    for k in ("gi_traces", "sphere_steps", "dda_steps", "csdf_checks", "tex_samples"):
-        assert out[0][k] == out[1][k] == out[2][k] > 0, k
 
 
 def test_render_frames_two_streams(rv, atlas, monkeypatch):

@@ -20,7 +20,7 @@ HIT = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("u", "<f4"), ("v", "<f
                 ("undef", "<i4"), ("sphere", "<i4"), ("dda", "<i4"), ("check", "<i4"), ("pad", "<i4")])
 
 
-VARIANTS = {"g1": 0, "g2": 1, "g4": 2, "g8": 3, "g1_reuse": 4, "sm_g1": 5, "sm_g4": 6}
+VARIANTS = {"g1": 0, "g2": 1, "g4": 2, "g8": 3, "g1_reuse": 4}
 
 
 @pytest.fixture(scope="module")

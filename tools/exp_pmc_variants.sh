@@ -20,12 +20,20 @@ for v in ${VARIANTS:-main}; do
 import csv, glob, json, sys, collections
 v, js, d = sys.argv[1:4]
 b = json.load(open(js))
-vals = collections.defaultdict(list)
+rows = []
 for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         if "k_ref_pipe" in row["Kernel_Name"] or "k_render" in row["Kernel_Name"]:
-            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+            rows.append(row)
+# the launches of the largest grid (full frame groups / whole pipelined frames)
+gmax = max(int(r.get("Grid_Size", 0)) for r in rows)
+vals = collections.defaultdict(list)
+for r in rows:
+    if int(r.get("Grid_Size", 0)) == gmax:
+        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 avg = {k: round(sum(x) / len(x) / 1024.0 * (2 if k == "FETCH_SIZE" else 1), 1) for k, x in vals.items() if x}
-print(v, "ms", b["ms_per_step"], "kernel", b["kernel_ms"]["primary"], "MB/launch", avg)
+fpl = b["frames_per_launch"].get("primary", 1)
+print(v, "ms", b["ms_per_step"], "kernel", b["kernel_ms"]["primary"], "frames/launch", fpl, "grid", gmax,
+      "MiB/launch", avg, "MiB/frame", {k: round(x / fpl, 2) for k, x in avg.items()})
 PY
 done
