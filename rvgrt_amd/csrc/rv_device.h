@@ -210,7 +210,7 @@ RV_HD uint32_t csdf_byte(uint32_t word, uint32_t cx) { return (word >> ((cx & 3u
 RV_HD uint32_t csdf_load(const World& w, uint32_t off) { return load_dword(w, off); }
 RV_HD uint32_t voxel_load(const World& w, uint32_t off) { return load_dword(w, off); }
 RV_HD uint32_t voxel_bit(const World&, uint32_t x, uint32_t y) { return voxel_bit(x, y); }
-RV_HD uint32_t gi_texel(const World& w, uint64_t idx) { return w.gi[idx]; }
+RV_HD uint32_t gi_texel(const World& w, uint32_t idx) { return w.gi[idx]; }
 
 // The reference's layouts (include/cumath.cuh:33-45, include/CoarseArray.cuh:
 // 9-21): bit idx = x | y<<lx | z<<(lx+ly) in uint32 words, CSDF bytes x
@@ -253,7 +253,21 @@ RV_HD uint32_t voxel_load(const LinearWorld& w, uint32_t off) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.bits) + off);
 }
 RV_HD uint32_t voxel_bit(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
-RV_HD uint32_t gi_texel(const LinearWorld& w, uint64_t idx) { return w.gi[idx]; }
+RV_HD uint32_t gi_texel(const LinearWorld& w, uint32_t idx) { return w.gi[idx]; }
+// GI grid (X/4 x Y/4 x Z/4, x fastest, power-of-two dims < 2^32 cells): log2 GX, log2 (GX * GY)
+RV_HD uint32_t gi_shift_x(const World& w) { return (uint32_t)w.lbx + 1u; }
+RV_HD uint32_t gi_shift_xy(const World& w) { return (uint32_t)w.lbxy + 2u; }
+RV_HD uint32_t gi_shift_x(const LinearWorld& w) { return (uint32_t)w.lx - 2u; }
+RV_HD uint32_t gi_shift_xy(const LinearWorld& w) { return (uint32_t)w.lxy - 4u; }
+// GI cell of a sample point (src/raytracing_functions.cu:247-251): truncating
+// casts (R11: -1..-3 -> 0), in-bounds test as one unsigned compare per axis,
+// the cell index from shifts
+template <class WV>
+RV_HD bool gi_cell_of(const WV& w, f3 p, uint32_t& idx) {
+    const int gx = (int)(floorf(p.x) / 4.0f), gy = (int)(floorf(p.y) / 4.0f), gz = (int)(floorf(p.z) / 4.0f);
+    idx = ((uint32_t)gz << gi_shift_xy(w)) | ((uint32_t)gy << gi_shift_x(w)) | (uint32_t)gx;
+    return ((uint32_t)gx < (uint32_t)w.GX) & ((uint32_t)gy < (uint32_t)w.GY) & ((uint32_t)gz < (uint32_t)w.GZ);
+}
 // addresses of a CSDF / voxel dword (gather diagnostics only)
 RV_HD const void* csdf_ptr(const World& w, uint32_t off) { return reinterpret_cast<const char*>(w.brick) + off; }
 RV_HD const void* csdf_ptr(const LinearWorld& w, uint32_t off) { return w.csdf + off; }
@@ -290,16 +304,17 @@ RV_HD uint32_t get_distance_i(const WV& w, int x, int y, int z) {
 
 // ---------------------------------------------------------------- noise
 // include/TerrainGeneration.cuh:25-44
-RV_HD uint32_t hash3(int xi, int yi, int zi) {
-    uint32_t key = (uint32_t)xi * 73856093u;
-    key ^= (uint32_t)yi * 19349663u;
-    key ^= (uint32_t)zi * 83492791u;
+static constexpr uint32_t HP1 = 73856093u, HP2 = 19349663u, HP3 = 83492791u;
+RV_HD uint32_t hash_mix(uint32_t key) {   // hash3 after the coordinate products
     key = (key ^ 61u) ^ (key >> 16);
     key *= 9u;
     key = key ^ (key >> 4);
     key *= 0x27d4eb2du;
     key = key ^ (key >> 15);
     return key;
+}
+RV_HD uint32_t hash3(int xi, int yi, int zi) {
+    return hash_mix(((uint32_t)xi * HP1) ^ ((uint32_t)yi * HP2) ^ ((uint32_t)zi * HP3));
 }
 RV_HD uint32_t hash2(int xi, int yi) {
     uint32_t key = (uint32_t)xi * 73856093u;
@@ -338,14 +353,19 @@ RV_HD float simplex3D(float px, float py, float pz) {
     float x1 = x0 - (float)i1 + G3, y1 = y0 - (float)j1 + G3, z1 = z0 - (float)k1 + G3;
     float x2 = x0 - (float)i2 + 2.0f * G3, y2 = y0 - (float)j2 + 2.0f * G3, z2 = z0 - (float)k2 + 2.0f * G3;
     float x3 = x0 - 1.0f + 3.0f * G3, y3 = y0 - 1.0f + 3.0f * G3, z3 = z0 - 1.0f + 3.0f * G3;
+    // the corners' hash3 products from the base corner's: (i + di) * P = i * P + di * P (mod 2^32),
+    // three integer multiplies per evaluation instead of twelve
+    const uint32_t A = (uint32_t)i * HP1, B = (uint32_t)j * HP2, C = (uint32_t)k * HP3;
     float t0 = 0.5f - x0 * x0 - y0 * y0 - z0 * z0; t0 = fmaxf(0.0f, t0); t0 *= t0;
-    float n0 = t0 * t0 * grad_dot3(hash3(i, j, k), x0, y0, z0);
+    float n0 = t0 * t0 * grad_dot3(hash_mix(A ^ B ^ C), x0, y0, z0);
     float t1 = 0.5f - x1 * x1 - y1 * y1 - z1 * z1; t1 = fmaxf(0.0f, t1); t1 *= t1;
-    float n1 = t1 * t1 * grad_dot3(hash3(i + i1, j + j1, k + k1), x1, y1, z1);
+    float n1 = t1 * t1 * grad_dot3(hash_mix((A + (i1 ? HP1 : 0u)) ^ (B + (j1 ? HP2 : 0u)) ^ (C + (k1 ? HP3 : 0u))),
+                                   x1, y1, z1);
     float t2 = 0.5f - x2 * x2 - y2 * y2 - z2 * z2; t2 = fmaxf(0.0f, t2); t2 *= t2;
-    float n2 = t2 * t2 * grad_dot3(hash3(i + i2, j + j2, k + k2), x2, y2, z2);
+    float n2 = t2 * t2 * grad_dot3(hash_mix((A + (i2 ? HP1 : 0u)) ^ (B + (j2 ? HP2 : 0u)) ^ (C + (k2 ? HP3 : 0u))),
+                                   x2, y2, z2);
     float t3 = 0.5f - x3 * x3 - y3 * y3 - z3 * z3; t3 = fmaxf(0.0f, t3); t3 *= t3;
-    float n3 = t3 * t3 * grad_dot3(hash3(i + 1, j + 1, k + 1), x3, y3, z3);
+    float n3 = t3 * t3 * grad_dot3(hash_mix((A + HP1) ^ (B + HP2) ^ (C + HP3)), x3, y3, z3);
     return 96.0f * (n0 + n1 + n2 + n3);
 }
 
@@ -442,6 +462,9 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 // Build-time defaults of the traversal variants (kernels pick per launch
 // shape, see rv_kernels.hip): G = DDA look-ahead group, REUSE = keep the last
 // gathered word of each phase and gather again only when its address moves.
+#ifndef RV_SPHERE_FORM
+#define RV_SPHERE_FORM 0
+#endif
 #ifndef RV_WORD_REUSE
 #define RV_WORD_REUSE 0
 #endif
@@ -488,11 +511,16 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             }
             if (COUNT) sc.sphere += !oob;
             const bool stop = oob | (d <= 1);
-            f3 nxt = add(cur, scale(dir, (float)d));
-            cur.x = stop ? cur.x : nxt.x;
-            cur.y = stop ? cur.y : nxt.y;
-            cur.z = stop ? cur.z : nxt.z;
-            if (stop) break;
+            if (RV_SPHERE_FORM == 1) {   // plain early exit: the loop-carried position needs no copies
+                if (stop) break;
+                cur = add(cur, scale(dir, (float)d));
+            } else {
+                f3 nxt = add(cur, scale(dir, (float)d));
+                cur.x = stop ? cur.x : nxt.x;
+                cur.y = stop ? cur.y : nxt.y;
+                cur.z = stop ? cur.z : nxt.z;
+                if (stop) break;
+            }
         }
         if (oob) {            // the reference's DDA then fails its bounds test at i = 0
             if (COUNT) sc.its++;
@@ -672,12 +700,10 @@ RV_HD f3 trace_cone(const WV& w, f3 pos, f3 dir, uint32_t& steps) {
         float scene = get_distance_f(w, p) * 2.0f;
         float width = cd * RV_TAN_CONE;
         if (scene < width) { alpha = 1.0f; continue; }
-        int gx = (int)(floorf(p.x) / 4.0f);
-        int gy = (int)(floorf(p.y) / 4.0f);
-        int gz = (int)(floorf(p.z) / 4.0f);
-        if (gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ) {
-            RV_GD(1, w.gi + ((uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx));
-            uint32_t s = gi_texel(w, (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx);
+        uint32_t gidx;
+        if (gi_cell_of(w, p, gidx)) {
+            RV_GD(1, w.gi + gidx);
+            uint32_t s = gi_texel(w, gidx);
             f3 c = V(u8f(s & 255u), u8f((s >> 8) & 255u),
                      u8f((s >> 16) & 255u));
             float a = u8f(s >> 24);
@@ -727,10 +753,9 @@ RV_HD f3 trace_cones6(const WV& w, f3 pos, f3 up, f3 right, f3 fwd, uint32_t& st
         for (int j = 0; j < CB; j++) {
             const f3 p = add(pos, scale(cone_dir(k0 + j, up, right, fwd), 3.0f));
             scene0[j] = get_distance_f(w, p) * 2.0f;
-            const int gx = (int)(floorf(p.x) / 4.0f), gy = (int)(floorf(p.y) / 4.0f), gz = (int)(floorf(p.z) / 4.0f);
-            in0[j] = gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ;
-            const uint64_t gi = in0[j] ? (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx : 0;
-            tex0[j] = gi_texel(w, gi);
+            uint32_t gidx;
+            in0[j] = gi_cell_of(w, p, gidx);
+            tex0[j] = gi_texel(w, in0[j] ? gidx : 0u);
         }
 #pragma unroll
         for (int j = 0; j < CB; j++) {
@@ -763,11 +788,9 @@ RV_HD f3 trace_cones6(const WV& w, f3 pos, f3 up, f3 right, f3 fwd, uint32_t& st
                 float scene = get_distance_f(w, p) * 2.0f;
                 float width = cd * RV_TAN_CONE;
                 if (scene < width) { alpha = 1.0f; continue; }
-                int gx = (int)(floorf(p.x) / 4.0f);
-                int gy = (int)(floorf(p.y) / 4.0f);
-                int gz = (int)(floorf(p.z) / 4.0f);
-                if (gx >= 0 && gx < w.GX && gy >= 0 && gy < w.GY && gz >= 0 && gz < w.GZ) {
-                    uint32_t s = gi_texel(w, (uint64_t)gz * (uint64_t)(w.GX * w.GY) + (uint64_t)gy * w.GX + gx);
+                uint32_t gidx;
+                if (gi_cell_of(w, p, gidx)) {
+                    uint32_t s = gi_texel(w, gidx);
                     f3 c = V(u8f(s & 255u), u8f((s >> 8) & 255u),
                              u8f((s >> 16) & 255u));
                     float a = u8f(s >> 24);

@@ -63,6 +63,11 @@ int rvh_variants(void) { return 5; }
 // rv::u8f, the device's byte -> float conversion
 float rvh_u8f(uint32_t b) { return rv::u8f(b); }
 
+// rv::simplex3D (texture and water noise, world build) over n points
+void rvh_simplex3D(const float* xyz, float* out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = rv::simplex3D(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+}
+
 int rvh_trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
                    const float* dir, const float* dist, int64_t n, HostHit* out) {
     Hit (*fn)(const World&, f3, f3, float, StepCount&) = nullptr;
