@@ -279,6 +279,44 @@ RV_HD uint32_t csdf_at(const WV& w, int cx, int cy, int cz) {
     return csdf_byte(csdf_load(w, csdf_off(w, (uint32_t)cx, (uint32_t)cy, (uint32_t)cz)), (uint32_t)cx);
 }
 
+// Coordinate-addressed dwords the traversal gathers (overloaded by WorldTile).
+template <class WV>
+RV_HD uint32_t csdf_word_at(const WV& w, uint32_t cx, uint32_t cy, uint32_t cz) {
+    return csdf_load(w, csdf_off(w, cx, cy, cz));
+}
+template <class WV>
+RV_HD uint32_t voxel_word_at(const WV& w, uint32_t x, uint32_t y, uint32_t z) {
+    return voxel_load(w, voxel_word_off(w, x, y, z));
+}
+
+// The brick layout with a wave's 2x2x2-brick tile (16^3 voxels: 512 B of bits,
+// 512 B of CSDF) staged in LDS (RV_PRIMARY_TILE): gathers that fall inside the
+// tile read LDS (~50-cycle latency) instead of the vector L1/L2 path; the rest
+// read the world.  The tile is wave-uniform (tbx.. from the wave's first lane).
+struct WorldTile : World {
+    const uint32_t* tile;   // LDS: [brick (k*2+j)*2+i][16 dwords] bits, then the same for the CSDF
+    uint32_t tbx, tby, tbz;
+};
+RV_HD bool tile_has(const WorldTile& w, uint32_t bx, uint32_t by, uint32_t bz, uint32_t& q) {
+    const uint32_t i = bx - w.tbx, j = by - w.tby, k = bz - w.tbz;
+    q = (((k << 1) | j) << 1) | i;
+    return (i | j | k) < 2u;
+}
+RV_HD uint32_t voxel_word_at(const WorldTile& w, uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t q;
+    if (tile_has(w, x >> 3, y >> 3, z >> 3, q)) return w.tile[q * 16u + (((y >> 2) & 1u) | ((z & 7u) << 1))];
+    return voxel_load(w, voxel_word_off(w, x, y, z));
+}
+RV_HD uint32_t csdf_word_at(const WorldTile& w, uint32_t cx, uint32_t cy, uint32_t cz) {
+    uint32_t q;
+    if (tile_has(w, cx >> 2, cy >> 2, cz >> 2, q))
+        return w.tile[128u + q * 16u + (((cy & 3u) >> 0) | ((cz & 3u) << 2))];
+    return csdf_load(w, csdf_off(w, cx, cy, cz));
+}
+RV_HD uint32_t csdf_at(const WorldTile& w, int cx, int cy, int cz) {
+    return csdf_byte(csdf_word_at(w, (uint32_t)cx, (uint32_t)cy, (uint32_t)cz), (uint32_t)cx);
+}
+
 // getDistance(float3) (include/raytracing_functions.cuh:35-51): truncating
 // cast after floorf*0.5, clamped to the grid (Appendix R11).
 template <class WV>
@@ -558,11 +596,11 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                         uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
                         uint32_t cz = (uint32_t)imin(imax(jz >> 1, 0), w.SZ - 1);
                         RV_GD(gd::CHECK, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
-                        cw = csdf_load(w, csdf_off(w, cx, cy, cz));
+                        cw = csdf_word_at(w, cx, cy, cz);
                     }
                     const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
                     RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
-                    wv[j] = voxel_load(w, voxel_word_off(w, qx, qy, qz));
+                    wv[j] = voxel_word_at(w, qx, qy, qz);
                     const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
                     const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
                     ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
@@ -619,7 +657,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 word = v_word;
             } else {
                 RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
-                word = voxel_load(w, voxel_word_off(w, qx, qy, qz));
+                word = voxel_word_at(w, qx, qy, qz);
             }
             const bool solid = (word >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
             if (COUNT) sc.dda += (st == 0) & !oob;
