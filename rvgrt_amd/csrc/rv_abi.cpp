@@ -278,7 +278,7 @@ f3 sun_dir() {
 
 World current_world(const rv_ctx* c) {
     World w = c->w;
-    w.brick = c->brick;
+    world_set_brick(w, c->brick);
     w.gi = c->gi;
     w.atlas = c->atlas;
     return w;
@@ -301,6 +301,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     // brick records must stay below 4 GiB (32-bit gather offsets): <= 2^34 voxels
     if (cfg->log2_x + cfg->log2_y + cfg->log2_z > 34) return RV_ERR_INVALID;
     if (cfg->width < 2 || cfg->height < 2 || (cfg->width & 1) || (cfg->height & 1)) return RV_ERR_INVALID;
+    if (cfg->width > 32768 || cfg->height > 32768) return RV_ERR_INVALID;   // images < 4 GiB: 32-bit offsets
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return RV_ERR_NO_DEVICE;
     hipDeviceProp_t prop;
@@ -1152,6 +1153,9 @@ rv_status rv_untile(rv_ctx* c, const void* dev_tiles, const int32_t* tile_ids, i
 rv_status rv_bind_output(rv_ctx* c, int32_t kind, void* p, size_t pitch) {
     if (!c) return RV_ERR_INVALID;
     size_t W = (size_t)c->cfg.width;
+    // the frame kernels address an image with a 32-bit byte offset from its base
+    if (p && (uint64_t)pitch * (uint64_t)c->cfg.height >= (1ull << 32))
+        return fail(c, RV_ERR_INVALID, "image larger than 4 GiB (pitch x height)");
     switch (kind) {
     case RV_IMAGE_COLOR:
         if (p && pitch < W * 4) return fail(c, RV_ERR_INVALID, "pitch too small");

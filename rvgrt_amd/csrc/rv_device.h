@@ -145,7 +145,14 @@ struct World {
     float fX, fY, fZ;
     int aw, ah;
     uint32_t coff;                       // byte offset of brick 0's 64 CSDF bytes
+    const uint32_t* __restrict__ csdf;   // = brick + coff: the CSDF region's own base, so a CSDF
+                                         // gather is SGPR base + the brick-relative offset
 };
+// Point a world view at its brick records (both region bases).
+RV_HD void world_set_brick(World& w, const uint32_t* brick) {
+    w.brick = brick;
+    w.csdf = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(brick) + w.coff);
+}
 
 // Brick storage.  RV_SPLIT_BRICKS=0: one 128-B record per 8^3 brick, 64 B of
 // bits then 64 B of CSDF (coff = 64).  RV_SPLIT_BRICKS=1: a bits region of
@@ -198,8 +205,9 @@ RV_HD bool is_solid(const World& w, int x, int y, int z) {
 
 // CSDF byte of an in-range coarse cell: the dword holding it, then the byte
 // (4x4x4 cells per record, byte = (cx&3) | (cy&3)<<2 | (cz&3)<<4 after 64 B of bits).
+// byte offset from World::csdf
 RV_HD uint32_t csdf_off(const World& w, uint32_t cx, uint32_t cy, uint32_t cz) {
-    return (brick_byte(w, cx >> 2, cy >> 2, cz >> 2) + w.coff) | ((cy & 3u) << 2) | ((cz & 3u) << 4);
+    return brick_byte(w, cx >> 2, cy >> 2, cz >> 2) | ((cy & 3u) << 2) | ((cz & 3u) << 4);
 }
 RV_HD uint32_t csdf_byte(uint32_t word, uint32_t cx) { return (word >> ((cx & 3u) << 3)) & 255u; }
 
@@ -207,7 +215,9 @@ RV_HD uint32_t csdf_byte(uint32_t word, uint32_t cx) { return (word >> ((cx & 3u
 // dword locator and its load for the CSDF and for the voxel bits, and the bit
 // of voxel (x, y) inside its word.  World = the brick layout above;
 // LinearWorld (below) = the reference's own layout.
-RV_HD uint32_t csdf_load(const World& w, uint32_t off) { return load_dword(w, off); }
+RV_HD uint32_t csdf_load(const World& w, uint32_t off) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.csdf) + off);
+}
 RV_HD uint32_t voxel_load(const World& w, uint32_t off) { return load_dword(w, off); }
 RV_HD uint32_t voxel_bit(const World&, uint32_t x, uint32_t y) { return voxel_bit(x, y); }
 RV_HD uint32_t gi_texel(const World& w, uint32_t idx) { return w.gi[idx]; }
@@ -269,7 +279,7 @@ RV_HD bool gi_cell_of(const WV& w, f3 p, uint32_t& idx) {
     return ((uint32_t)gx < (uint32_t)w.GX) & ((uint32_t)gy < (uint32_t)w.GY) & ((uint32_t)gz < (uint32_t)w.GZ);
 }
 // addresses of a CSDF / voxel dword (gather diagnostics only)
-RV_HD const void* csdf_ptr(const World& w, uint32_t off) { return reinterpret_cast<const char*>(w.brick) + off; }
+RV_HD const void* csdf_ptr(const World& w, uint32_t off) { return reinterpret_cast<const char*>(w.csdf) + off; }
 RV_HD const void* csdf_ptr(const LinearWorld& w, uint32_t off) { return w.csdf + off; }
 RV_HD const void* voxel_ptr(const World& w, uint32_t off) { return reinterpret_cast<const char*>(w.brick) + off; }
 RV_HD const void* voxel_ptr(const LinearWorld& w, uint32_t off) { return reinterpret_cast<const char*>(w.bits) + off; }
@@ -865,16 +875,16 @@ RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
                          floorf((float)((double)pos.z + 721.5)) * freq * 0.3f);
     e = e * 0.4f + e2 * 0.6f;
     }
-    int tile;  // (bx,by) in 1/16 units
-    if (e < -1.3f) tile = 0x10;        // stone   (0,1)
-    else if (e < -1.2f) tile = 0x23;   // diamond (3,2)
-    else if (e < -0.7f) tile = 0x12;   // iron    (2,1)
-    else if (e < 0.0f) tile = 0x10;    // stone
-    else if (e < 0.1f) tile = 0x22;    // coal    (2,2)
-    else if (e < 0.4f) tile = 0x01;    // cobble  (1,0)
-    else if (e < 0.8f) tile = 0x20;    // dirt    (0,2)
-    else if (e < 1.2f) tile = 0x00;    // stone2  (0,0)
-    else tile = 0x10;                  // stone
+    // (bx,by) in 1/16 units: the first threshold e is below, as a select chain (no branches)
+    int tile = 0x10;                   // stone
+    tile = e < 1.2f ? 0x00 : tile;     // stone2  (0,0)
+    tile = e < 0.8f ? 0x20 : tile;     // dirt    (0,2)
+    tile = e < 0.4f ? 0x01 : tile;     // cobble  (1,0)
+    tile = e < 0.1f ? 0x22 : tile;     // coal    (2,2)
+    tile = e < 0.0f ? 0x10 : tile;     // stone
+    tile = e < -0.7f ? 0x12 : tile;    // iron    (2,1)
+    tile = e < -1.2f ? 0x23 : tile;    // diamond (3,2)
+    tile = e < -1.3f ? 0x10 : tile;    // stone   (0,1)
     float bx = (float)(tile & 15) * (1.0f / 16.0f), by = (float)(tile >> 4) * (1.0f / 16.0f);
     float ux = hround(hround(u * 0.0625f) + bx);
     float uy = hround(hround(v * 0.0625f) + by);
@@ -883,7 +893,8 @@ RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
     int row = imin((int)floorf(cv * (float)w.ah), w.ah - 1);
     RV_GD_KIND(gd::TEX);
     RV_GD(0, w.atlas + row * w.aw + col);
-    uint32_t t = w.atlas[row * w.aw + col];
+    const uint32_t t = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.atlas) +
+                                                          4u * (uint32_t)(row * w.aw + col));
     return V(u8f(t & 255u), u8f((t >> 8) & 255u),
              u8f((t >> 16) & 255u));
 }

@@ -46,7 +46,7 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
                 uint32_t local = (uint32_t)((cx & 3) | ((cy & 3) << 2) | ((cz & 3) << 4));
                 bytes[csdf_byte_index(w.coff, b, local)] = csdf[(cz * w.SY + cy) * w.SX + cx];
             }
-    w.brick = h.brick.data();
+    world_set_brick(w, h.brick.data());
 }
 template <int G, bool REUSE>
 Hit trace_v(const World& w, f3 o, f3 d, float t, StepCount& sc) { return trace<true, G, REUSE>(w, o, d, t, sc); }
