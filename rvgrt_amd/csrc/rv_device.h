@@ -510,6 +510,9 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 // Build-time defaults of the traversal variants (kernels pick per launch
 // shape, see rv_kernels.hip): G = DDA look-ahead group, REUSE = keep the last
 // gathered word of each phase and gather again only when its address moves.
+#ifndef RV_DDA_NOBREAK   // look-ahead groups replayed without an early exit (predicated steps)
+#define RV_DDA_NOBREAK 0
+#endif
 #ifndef RV_SPHERE_FORM
 #define RV_SPHERE_FORM 0
 #endif
@@ -619,12 +622,24 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             }
 #pragma unroll
             for (int j = 0; j < G; j++) {
+                if (RV_DDA_NOBREAK) {   // every step of the group runs, predicated on st == 0
+                    const bool g0 = st == 0;
+                    if (COUNT) sc.its += g0;
+                    if (j == G - 1 && chk) {
+                        uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
+                        const uint32_t jd1 = csdf_byte(cw, cx);
+                        if (COUNT) sc.check += g0;
+                        jd = g0 ? jd1 : jd;
+                        st = g0 ? (jd1 > 2 ? 1 : 0) : st;
+                    }
+                } else {
                 if (COUNT) sc.its++;
                 if (j == G - 1 && chk) {
                     uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
                     jd = csdf_byte(cw, cx);
                     if (COUNT) sc.check++;
                     st = jd > 2 ? 1 : 0;
+                }
                 }
                 const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
                 const bool solid = (wv[j] >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
@@ -642,8 +657,9 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 iy += sely ? sy : 0;
                 iz += selz ? sz : 0;
                 mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
-                if (!go) { run = false; break; }
+                if (!RV_DDA_NOBREAK && !go) { run = false; break; }
             }
+            if (RV_DDA_NOBREAK && st != 0) run = false;
         }
         } else {
         for (int i = 0; i < 200; i++) {
