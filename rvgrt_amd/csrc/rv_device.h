@@ -510,8 +510,8 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 // Build-time defaults of the traversal variants (kernels pick per launch
 // shape, see rv_kernels.hip): G = DDA look-ahead group, REUSE = keep the last
 // gathered word of each phase and gather again only when its address moves.
-#ifndef RV_DDA_NOBREAK   // look-ahead groups replayed without an early exit (predicated steps)
-#define RV_DDA_NOBREAK 0
+#ifndef RV_DDA_REWALK    // look-ahead groups: stop search + re-walk of the stopping group (G > 1)
+#define RV_DDA_REWALK 1
 #endif
 #ifndef RV_SPHERE_FORM
 #define RV_SPHERE_FORM 0
@@ -520,10 +520,10 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 #define RV_WORD_REUSE 0
 #endif
 
-// NB: a look-ahead group's replay runs all G steps predicated on "still walking" instead of
-// leaving at the stopping step (fewer exec-mask branches, a few more VALU): C3's latency-bound
-// pre-pass and GI rays -4.6 %, C4's throughput-bound render +1 % -- so it is chosen per ray kind.
-template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0), bool NB = (RV_DDA_NOBREAK != 0),
+// RW: look-ahead groups by stop search + re-walk (default) or by the step-by-step replay with an
+// early exit (round 1-2; kept for A/B and checked bit-exact on the CPU, tests/test_host_trace.py).
+// Re-walk: C4 0.667 -> 0.631 ms, C3 0.282 -> 0.270 (profiles/r02/rewalk_ab.txt).
+template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0), bool RW = (RV_DDA_REWALK != 0),
           class WV = World>
 RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
@@ -590,7 +590,89 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         mask = -128;
         int st = 0;           // 1: jump, 2: out of bounds, 3: hit
         uint32_t jd = 0;
-        if constexpr (G > 1) {
+        if constexpr (G > 1 && RW) {
+        // Look-ahead, stop search + re-walk.  The walk of a group visits the G cells the DDA would
+        // visit if it did not stop (data-independent), gathers their words and, per cell, the mask
+        // of its bit (0 for a cell outside the grid).  The stop search is then an AND, two compares
+        // and a select per step: the first cell whose word meets its mask or that lies outside, or
+        // the group's check.
+        // Only where a lane stops are its k < G steps walked again from the group start, so the
+        // per-step selection and state updates run once per step instead of twice.
+        static_assert(G == 2 || G == 4 || G == 8, "the look-ahead group divides 8");
+        int kk = G;           // stop step inside the stopping group (G: no stop)
+        bool jmp = false;
+        for (int i0 = 0; i0 < 200; i0 += G) {
+            uint32_t wv[G], bm[G];
+            uint32_t cw = 0, ccx = 0;
+            const bool chk = ((i0 + G - 1) & 7) == 7;   // wave-uniform
+            int jx = ix, jy = iy, jz = iz, jm = mask;
+            float ux = tx, uy = ty, uz = tz;
+#pragma unroll
+            for (int j = 0; j < G; j++) {
+                const bool ob = ((uint32_t)jx >= X) | ((uint32_t)jy >= Y) | ((uint32_t)jz >= Z);
+                const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
+                RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
+                wv[j] = voxel_word_at(w, qx, qy, qz);
+                if (j == G - 1 && chk) {   // after the last voxel gather: all G + 1 loads in flight
+                    const uint32_t cx = (uint32_t)imin(imax(jx >> 1, 0), w.SX - 1);
+                    const uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
+                    const uint32_t cz = (uint32_t)imin(imax(jz >> 1, 0), w.SZ - 1);
+                    RV_GD(gd::CHECK, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
+                    cw = csdf_word_at(w, cx, cy, cz);
+                    ccx = cx;
+                }
+                bm[j] = ob ? 0u : (1u << voxel_bit(w, (uint32_t)jx, (uint32_t)jy));   // 0: outside
+                const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
+                const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
+                ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
+                jx += selx ? sx : 0; jy += sely ? sy : 0; jz += selz ? sz : 0;
+                if (j == G - 1) jm = selx ? 0 : (sely ? 1 : 2);
+            }
+            int k = G;
+            const uint32_t jd1 = csdf_byte(cw, ccx);   // 0 in a group without a check
+            const bool jp = jd1 > 2;
+#pragma unroll
+            for (int j = G - 1; j >= 0; j--) {
+                bool stop = ((wv[j] & bm[j]) != 0u) | (bm[j] == 0u);
+                if (j == G - 1) stop = stop | jp;
+                k = stop ? j : k;
+            }
+            if (k < G) {
+                kk = k;
+                jmp = jp & (k == G - 1);
+                jd = jd1;
+                if (COUNT) {
+                    sc.its += (uint32_t)k + 1u;
+                    sc.dda += (uint32_t)k;   // the stopping step's own count is settled below
+                    sc.check += (chk & (k == G - 1)) ? 1u : 0u;
+                }
+                break;
+            }
+            if (COUNT) { sc.its += G; sc.dda += G; sc.check += chk ? 1u : 0u; }
+            ix = jx; iy = jy; iz = jz; tx = ux; ty = uy; tz = uz; mask = jm;
+        }
+        if (kk < G) {
+            // the stopping group again from its start, kk steps: the state at the stopping cell
+#pragma unroll
+            for (int j = 0; j < G - 1; j++) {
+                const bool go = j < kk;
+                const bool cxy = tx < ty, cxz = tx < tz, cyz = ty < tz;
+                const bool selx = go & cxy & cxz;
+                const bool sely = go & !cxy & cyz;
+                const bool selz = go & !(cxy & cxz) & !(!cxy & cyz);
+                tx = selx ? tx + ddx : tx;
+                ty = sely ? ty + ddy : ty;
+                tz = selz ? tz + ddz : tz;
+                ix += selx ? sx : 0;
+                iy += sely ? sy : 0;
+                iz += selz ? sz : 0;
+                mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
+            }
+            const bool ob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
+            st = jmp ? 1 : (ob ? 2 : 3);
+            if (COUNT) sc.dda += st == 3 ? 1u : 0u;
+        }
+        } else if constexpr (G > 1) {
         // Look-ahead: the cells a DDA walk visits do not depend on the data
         // it reads (only where it stops does), so the next G cells' words --
         // and the CSDF word of an every-8th-step check among them -- are
@@ -626,24 +708,12 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             }
 #pragma unroll
             for (int j = 0; j < G; j++) {
-                if (NB) {   // every step of the group runs, predicated on st == 0
-                    const bool g0 = st == 0;
-                    if (COUNT) sc.its += g0;
-                    if (j == G - 1 && chk) {
-                        uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
-                        const uint32_t jd1 = csdf_byte(cw, cx);
-                        if (COUNT) sc.check += g0;
-                        jd = g0 ? jd1 : jd;
-                        st = g0 ? (jd1 > 2 ? 1 : 0) : st;
-                    }
-                } else {
                 if (COUNT) sc.its++;
                 if (j == G - 1 && chk) {
                     uint32_t cx = (uint32_t)imin(imax(ix >> 1, 0), w.SX - 1);
                     jd = csdf_byte(cw, cx);
                     if (COUNT) sc.check++;
                     st = jd > 2 ? 1 : 0;
-                }
                 }
                 const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
                 const bool solid = (wv[j] >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
@@ -661,9 +731,8 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 iy += sely ? sy : 0;
                 iz += selz ? sz : 0;
                 mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
-                if (!NB && !go) { run = false; break; }
+                if (!go) { run = false; break; }
             }
-            if (NB && st != 0) run = false;
         }
         } else {
         for (int i = 0; i < 200; i++) {

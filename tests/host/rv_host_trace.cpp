@@ -48,8 +48,8 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
             }
     world_set_brick(w, h.brick.data());
 }
-template <int G, bool REUSE, bool NB = false>
-Hit trace_v(const World& w, f3 o, f3 d, float t, StepCount& sc) { return trace<true, G, REUSE, NB>(w, o, d, t, sc); }
+template <int G, bool REUSE, bool RW = true>
+Hit trace_v(const World& w, f3 o, f3 d, float t, StepCount& sc) { return trace<true, G, REUSE, RW>(w, o, d, t, sc); }
 }  // namespace
 
 extern "C" {
@@ -57,8 +57,8 @@ extern "C" {
 // Out record per ray (48 B): pos[3], normal[3], u, v, hit, undef, sphere, dda, check (ints)
 struct HostHit { float pos[3], normal[3], u, v; int32_t hit, undef, sphere, dda, check, pad; };
 
-// variant: 0..3 = DDA look-ahead group 1/2/4/8, 4 = group 1 with word reuse,
-// 5..6 = group 4 / 8 with the predicated replay (trace NB)
+// variant: 0..3 = DDA look-ahead group 1/2/4/8 (stop search + re-walk), 4 = group 1 with word
+// reuse, 5..6 = group 4 / 8 with the step-by-step replay (trace RW = false)
 int rvh_variants(void) { return 7; }
 
 // rv::u8f, the device's byte -> float conversion
@@ -78,8 +78,8 @@ int rvh_trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, co
     case 2: fn = trace_v<4, false>; break;
     case 3: fn = trace_v<8, false>; break;
     case 4: fn = trace_v<1, true>; break;
-    case 5: fn = trace_v<4, false, true>; break;
-    case 6: fn = trace_v<8, false, true>; break;
+    case 5: fn = trace_v<4, false, false>; break;
+    case 6: fn = trace_v<8, false, false>; break;
     default: return -1;
     }
     HostWorld h;

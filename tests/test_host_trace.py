@@ -2,7 +2,7 @@
 the CPU (tests/host/rv_host_trace.cpp) against the oracle: hit, position,
 normal, uv and sphere/DDA/check step counts bit-exact on random rays, for
 every traversal variant the GPU kernels can select (DDA look-ahead group
-1/2/4/8, word reuse, predicated look-ahead replay).
+1/2/4/8 by stop search + re-walk, word reuse, the step-by-step replay).
 Runs without a GPU; the GPU build of the same source is checked by
 tests/test_gpu_parity.py::test_trace_bit_exact."""
 import ctypes as C
@@ -20,7 +20,7 @@ HIT = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("u", "<f4"), ("v", "<f
                 ("undef", "<i4"), ("sphere", "<i4"), ("dda", "<i4"), ("check", "<i4"), ("pad", "<i4")])
 
 
-VARIANTS = {"g1": 0, "g2": 1, "g4": 2, "g8": 3, "g1_reuse": 4, "g4_nb": 5, "g8_nb": 6}
+VARIANTS = {"g1": 0, "g2": 1, "g4": 2, "g8": 3, "g1_reuse": 4, "g4_replay": 5, "g8_replay": 6}
 
 
 @pytest.fixture(scope="module")
