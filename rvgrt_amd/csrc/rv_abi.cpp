@@ -317,11 +317,12 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     World& w = c->w;
     w.X = 1 << c->lx; w.Y = 1 << c->ly; w.Z = 1 << c->lz;
     w.lbx = c->lx - 3; w.lbxy = (c->lx - 3) + (c->ly - 3);
+    w.lbz = c->lz - 3; w.lbzy = (c->lz - 3) + (c->ly - 3);
     w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
     w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
     c->brick_bytes = ((uint64_t)w.X * w.Y * w.Z) / 4;   // 128 B per 512 voxels
-    w.coff = csdf_region(((uint64_t)w.X * w.Y * w.Z) / 512);
+    world_set_regions(w, ((uint64_t)w.X * w.Y * w.Z) / 512);
     c->gi_bytes = n_gi(c) * 4;
 
     auto cleanup_fail = [&](rv_status s, const char* what) {

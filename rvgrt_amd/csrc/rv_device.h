@@ -139,12 +139,14 @@ struct World {
     const uint32_t* __restrict__ gi;     // RGBA8 per 4^3 cell, x fastest
     const uint32_t* __restrict__ atlas;  // RGBA8 atlas, row-major
     int X, Y, Z;                         // voxel dims
-    int lbx, lbxy;                       // brick id = bx | by<<lbx | bz<<lbxy
+    int lbx, lbxy;                       // log2 bricks along x, along x*y (the GI grid's shifts)
+    int lbz, lbzy;                       // brick id = bz | by<<lbz | bx<<lbzy (z fastest, see brick_of)
     int SX, SY, SZ;                      // CSDF dims (X/2 ...)
     int GX, GY, GZ;                      // GI dims (X/4 ...)
     float fX, fY, fZ;
     int aw, ah;
     uint32_t coff;                       // byte offset of brick 0's 64 CSDF bytes
+    uint32_t omax;                       // last dword offset valid in both regions (world_set_regions)
     const uint32_t* __restrict__ csdf;   // = brick + coff: the CSDF region's own base, so a CSDF
                                          // gather is SGPR base + the brick-relative offset
 };
@@ -169,21 +171,37 @@ RV_HD void world_set_brick(World& w, const uint32_t* brick) {
 #endif
 static constexpr uint32_t BRICK_SHIFT = RV_SPLIT_BRICKS ? 6 : 7;   // log2 bytes between bricks
 __host__ __device__ inline uint32_t csdf_region(uint64_t nbricks) { return RV_SPLIT_BRICKS ? (uint32_t)(nbricks * 64) : 64u; }
+// Region geometry of a world of nbricks bricks: the CSDF region's offset and the last dword
+// offset that is valid from both region bases (the unclamped traversal gathers clamp to it).
+__host__ __device__ inline void world_set_regions(World& w, uint64_t nbricks) {
+    w.coff = csdf_region(nbricks);
+    w.omax = (uint32_t)(nbricks * (RV_SPLIT_BRICKS ? 64u : 128u) - (RV_SPLIT_BRICKS ? 4u : 68u));
+}
 // dword index of bit word wd (0..15) / byte index of CSDF byte `local` of brick b
 __host__ __device__ inline uint64_t bits_word_index(uint64_t b, uint32_t wd) { return (b << (BRICK_SHIFT - 2)) + wd; }
 __host__ __device__ inline uint64_t csdf_byte_index(uint32_t coff, uint64_t b, uint32_t local) {
     return (uint64_t)coff + (b << BRICK_SHIFT) + local;
 }
 
+// Bricks are ordered z fastest: the brick's z index sits right above the in-brick offset, whose
+// top field is the voxel's (bits: z & 7 at bits 3-5 of the dword offset; CSDF: cz & 3 at bits
+// 4-5), so a coordinate's z contribution to a gather offset is one shift (z << 3, cz << 4)
+// instead of two masked, shifted fields (DDA cell offset 11 -> 6 VALU).
+static_assert(RV_SPLIT_BRICKS, "the z-contiguous gather offsets assume 64-B brick regions");
 RV_HD uint64_t brick_of(const World& w, int bx, int by, int bz) {
-    return (uint64_t)(uint32_t)bx | ((uint64_t)(uint32_t)by << w.lbx) | ((uint64_t)(uint32_t)bz << w.lbxy);
+    return (uint64_t)(uint32_t)bz | ((uint64_t)(uint32_t)by << w.lbz) | ((uint64_t)(uint32_t)bx << w.lbzy);
+}
+RV_HD void brick_coords(const World& w, uint64_t b, uint32_t& bx, uint32_t& by, uint32_t& bz) {
+    bz = (uint32_t)(b & ((1ull << w.lbz) - 1));
+    by = (uint32_t)((b >> w.lbz) & ((1ull << (w.lbzy - w.lbz)) - 1));
+    bx = (uint32_t)(b >> w.lbzy);
 }
 
 // Byte offset of brick record (bx,by,bz).  The brick array is < 4 GiB
 // (rv_create caps worlds at 2^34 voxels), so offsets stay 32-bit and loads
 // use the SGPR-base + 32-bit VGPR-offset form (no 64-bit address math).
 RV_HD uint32_t brick_byte(const World& w, uint32_t bx, uint32_t by, uint32_t bz) {
-    return (bx << BRICK_SHIFT) | (by << (w.lbx + BRICK_SHIFT)) | (bz << (w.lbxy + BRICK_SHIFT));
+    return (bz << BRICK_SHIFT) | (by << (w.lbz + BRICK_SHIFT)) | (bx << (w.lbzy + BRICK_SHIFT));
 }
 RV_HD uint32_t load_dword(const World& w, uint32_t byte_off) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + byte_off);
@@ -192,7 +210,8 @@ RV_HD uint32_t load_dword(const World& w, uint32_t byte_off) {
 // Bit-word offset of voxel (x,y,z) and the bit inside it: within a brick
 // bit = (x&7) | (y&7)<<3 | (z&7)<<6, dword = bit>>5 = (y>>2 & 1) | (z&7)<<1.
 RV_HD uint32_t voxel_word_off(const World& w, uint32_t x, uint32_t y, uint32_t z) {
-    return brick_byte(w, x >> 3, y >> 3, z >> 3) | ((y & 4u) << 0) | ((z & 7u) << 3);
+    // = brick_byte(x >> 3, y >> 3, z >> 3) | (y & 4) | (z & 7) << 3 for in-range coordinates
+    return (z << 3) | (y & 4u) | ((y >> 3) << (w.lbz + BRICK_SHIFT)) | ((x >> 3) << (w.lbzy + BRICK_SHIFT));
 }
 RV_HD uint32_t voxel_bit(uint32_t x, uint32_t y) { return (x & 7u) | ((y & 3u) << 3); }
 
@@ -207,7 +226,8 @@ RV_HD bool is_solid(const World& w, int x, int y, int z) {
 // (4x4x4 cells per record, byte = (cx&3) | (cy&3)<<2 | (cz&3)<<4 after 64 B of bits).
 // byte offset from World::csdf
 RV_HD uint32_t csdf_off(const World& w, uint32_t cx, uint32_t cy, uint32_t cz) {
-    return brick_byte(w, cx >> 2, cy >> 2, cz >> 2) | ((cy & 3u) << 2) | ((cz & 3u) << 4);
+    // = brick_byte(cx >> 2, cy >> 2, cz >> 2) | (cy & 3) << 2 | (cz & 3) << 4 for in-range cells
+    return (cz << 4) | ((cy & 3u) << 2) | ((cy >> 2) << (w.lbz + BRICK_SHIFT)) | ((cx >> 2) << (w.lbzy + BRICK_SHIFT));
 }
 RV_HD uint32_t csdf_byte(uint32_t word, uint32_t cx) { return (word >> ((cx & 3u) << 3)) & 255u; }
 
@@ -220,6 +240,8 @@ RV_HD uint32_t csdf_load(const World& w, uint32_t off) {
 }
 RV_HD uint32_t voxel_load(const World& w, uint32_t off) { return load_dword(w, off); }
 RV_HD uint32_t voxel_bit(const World&, uint32_t x, uint32_t y) { return voxel_bit(x, y); }
+// a shift whose low 5 bits are voxel_bit (the hardware shift reads only those: one op fewer)
+RV_HD uint32_t voxel_shift(const World&, uint32_t x, uint32_t y) { return (x & 7u) | (y << 3); }
 RV_HD uint32_t gi_texel(const World& w, uint32_t idx) { return w.gi[idx]; }
 
 // The reference's layouts (include/cumath.cuh:33-45, include/CoarseArray.cuh:
@@ -263,6 +285,7 @@ RV_HD uint32_t voxel_load(const LinearWorld& w, uint32_t off) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.bits) + off);
 }
 RV_HD uint32_t voxel_bit(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
+RV_HD uint32_t voxel_shift(const LinearWorld&, uint32_t x, uint32_t) { return x; }
 RV_HD uint32_t gi_texel(const LinearWorld& w, uint32_t idx) { return w.gi[idx]; }
 // GI grid (X/4 x Y/4 x Z/4, x fastest, power-of-two dims < 2^32 cells): log2 GX, log2 (GX * GY)
 RV_HD uint32_t gi_shift_x(const World& w) { return (uint32_t)w.lbx + 1u; }
@@ -299,6 +322,42 @@ RV_HD uint32_t voxel_word_at(const WV& w, uint32_t x, uint32_t y, uint32_t z) {
     return voxel_load(w, voxel_word_off(w, x, y, z));
 }
 
+// (int)floorf(x) in one instruction on gfx950 (v_cvt_flr_i32_f32; the compiler only forms it
+// under no-NaN fast math).  Equal to floor + convert for every non-NaN input, denormals included.
+RV_HD int floor_i(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return (int)floorf(x);
+#endif
+}
+
+// Unclamped traversal gathers.  The sphere step and the DDA cell read the world only for
+// in-range coordinates (the reference tests bounds first; a lane outside the grid stops and its
+// value is unused), so the per-axis clamps that kept every lane's address valid are replaced by
+// one clamp of the finished offset: out-of-range coordinates alias some in-region dword.
+// The sphere step's CSDF byte is loaded as a byte (its position in the dword folded into the
+// offset).  Coordinates are the voxel's, as unsigned.
+RV_HD uint32_t csdf_step_byte(const World& w, uint32_t fx, uint32_t fy, uint32_t fz) {
+    const uint32_t off = ((fz >> 1) << 4) | ((fy << 1) & 12u) | ((fy >> 3) << (w.lbz + BRICK_SHIFT)) |
+                         ((fx >> 1) & 3u) | ((fx >> 3) << (w.lbzy + BRICK_SHIFT));
+    return *(reinterpret_cast<const uint8_t*>(w.csdf) + umin(off, w.omax + 3u));
+}
+RV_HD uint32_t csdf_step_byte(const LinearWorld& w, uint32_t fx, uint32_t fy, uint32_t fz) {
+    const uint32_t cx = umin(fx >> 1, (uint32_t)w.SX - 1u), cy = umin(fy >> 1, (uint32_t)w.SY - 1u),
+                   cz = umin(fz >> 1, (uint32_t)w.SZ - 1u);
+    return csdf_byte(csdf_load(w, csdf_off(w, cx, cy, cz)), cx);
+}
+RV_HD uint32_t voxel_word_nc(const World& w, uint32_t x, uint32_t y, uint32_t z) {
+    return load_dword(w, umin(voxel_word_off(w, x, y, z), w.omax));
+}
+RV_HD uint32_t voxel_word_nc(const LinearWorld& w, uint32_t x, uint32_t y, uint32_t z) {
+    return voxel_load(w, voxel_word_off(w, umin(x, (uint32_t)w.X - 1u), umin(y, (uint32_t)w.Y - 1u),
+                                        umin(z, (uint32_t)w.Z - 1u)));
+}
+
 // The brick layout with a wave's 2x2x2-brick tile (16^3 voxels: 512 B of bits,
 // 512 B of CSDF) staged in LDS (RV_PRIMARY_TILE): gathers that fall inside the
 // tile read LDS (~50-cycle latency) instead of the vector L1/L2 path; the rest
@@ -322,6 +381,17 @@ RV_HD uint32_t csdf_word_at(const WorldTile& w, uint32_t cx, uint32_t cy, uint32
     if (tile_has(w, cx >> 2, cy >> 2, cz >> 2, q))
         return w.tile[128u + q * 16u + (((cy & 3u) >> 0) | ((cz & 3u) << 2))];
     return csdf_load(w, csdf_off(w, cx, cy, cz));
+}
+RV_HD uint32_t voxel_word_nc(const WorldTile& w, uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t q;
+    if (tile_has(w, x >> 3, y >> 3, z >> 3, q)) return w.tile[q * 16u + (((y >> 2) & 1u) | ((z & 7u) << 1))];
+    return voxel_word_nc(static_cast<const World&>(w), x, y, z);
+}
+RV_HD uint32_t csdf_step_byte(const WorldTile& w, uint32_t fx, uint32_t fy, uint32_t fz) {
+    uint32_t q;
+    if (tile_has(w, fx >> 3, fy >> 3, fz >> 3, q))
+        return csdf_byte(w.tile[128u + q * 16u + (((fy >> 1) & 3u) | (((fz >> 1) & 3u) << 2))], fx >> 1);
+    return csdf_step_byte(static_cast<const World&>(w), fx, fy, fz);
 }
 RV_HD uint32_t csdf_at(const WorldTile& w, int cx, int cy, int cz) {
     return csdf_byte(csdf_word_at(w, (uint32_t)cx, (uint32_t)cy, (uint32_t)cz), (uint32_t)cx);
@@ -550,19 +620,21 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         // with a single exit, so a wave pays no divergent-branch bookkeeping.
         bool oob = false;
         for (int it = 0; it < 100; it++) {
-            int fx = (int)floorf(cur.x), fy = (int)floorf(cur.y), fz = (int)floorf(cur.z);
+            const int fx = floor_i(cur.x), fy = floor_i(cur.y), fz = floor_i(cur.z);
             oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= Y) | ((uint32_t)fz >= Z);
-            const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
-            const uint32_t cy = umin((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
-            const uint32_t cz = umin((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
             uint32_t d;
             if (REUSE) {   // gather only where the CSDF dword changed
+                const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
+                const uint32_t cy = umin((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u);
+                const uint32_t cz = umin((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u);
                 const uint32_t off = csdf_off(w, cx, cy, cz);
                 if (off != c_off) { c_word = csdf_load(w, off); c_off = off; }
                 d = csdf_byte(c_word, cx);
-            } else {
-                RV_GD(gd::SPHERE, csdf_ptr(w, csdf_off(w, cx, cy, cz)));
-                d = csdf_at(w, (int)cx, (int)cy, (int)cz);
+            } else {   // unclamped: an out-of-range lane stops and ignores its byte
+                RV_GD(gd::SPHERE, csdf_ptr(w, csdf_off(w, umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u),
+                                                       umin((uint32_t)(fy >> 1), (uint32_t)w.SY - 1u),
+                                                       umin((uint32_t)(fz >> 1), (uint32_t)w.SZ - 1u))));
+                d = csdf_step_byte(w, (uint32_t)fx, (uint32_t)fy, (uint32_t)fz);
             }
             if (COUNT) sc.sphere += !oob;
             const bool stop = oob | (d <= 1);
@@ -583,7 +655,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             break;
         }
         // ---- DDA set-up
-        ix = (int)floorf(cur.x); iy = (int)floorf(cur.y); iz = (int)floorf(cur.z);
+        ix = floor_i(cur.x); iy = floor_i(cur.y); iz = floor_i(cur.z);
         tx = ((sx > 0) ? ((float)ix + 1.0f - cur.x) : (cur.x - (float)ix)) * ddx;
         ty = ((sy > 0) ? ((float)iy + 1.0f - cur.y) : (cur.y - (float)iy)) * ddy;
         tz = ((sz > 0) ? ((float)iz + 1.0f - cur.z) : (cur.z - (float)iz)) * ddz;
@@ -592,9 +664,9 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         uint32_t jd = 0;
         if constexpr (G > 1 && RW) {
         // Look-ahead, stop search + re-walk.  The walk of a group visits the G cells the DDA would
-        // visit if it did not stop (data-independent), gathers their words and, per cell, the mask
-        // of its bit (0 for a cell outside the grid).  The stop search is then an AND, two compares
-        // and a select per step: the first cell whose word meets its mask or that lies outside, or
+        // visit if it did not stop (data-independent), gathers their words and, per cell, its bit's
+        // shift and whether it lies outside the grid.  The stop search is then a bit extract, a
+        // compare and a select per step: the first cell whose bit is set or that lies outside, or
         // the group's check.
         // Only where a lane stops are its k < G steps walked again from the group start, so the
         // per-step selection and state updates run once per step instead of twice.
@@ -602,7 +674,8 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         int kk = G;           // stop step inside the stopping group (G: no stop)
         bool jmp = false;
         for (int i0 = 0; i0 < 200; i0 += G) {
-            uint32_t wv[G], bm[G];
+            uint32_t wv[G], sh[G];
+            bool obv[G];
             uint32_t cw = 0, ccx = 0;
             const bool chk = ((i0 + G - 1) & 7) == 7;   // wave-uniform
             int jx = ix, jy = iy, jz = iz, jm = mask;
@@ -610,9 +683,9 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
 #pragma unroll
             for (int j = 0; j < G; j++) {
                 const bool ob = ((uint32_t)jx >= X) | ((uint32_t)jy >= Y) | ((uint32_t)jz >= Z);
-                const uint32_t qx = umin((uint32_t)jx, X - 1u), qy = umin((uint32_t)jy, Y - 1u), qz = umin((uint32_t)jz, Z - 1u);
-                RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
-                wv[j] = voxel_word_at(w, qx, qy, qz);
+                RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, umin((uint32_t)jx, X - 1u), umin((uint32_t)jy, Y - 1u),
+                                                           umin((uint32_t)jz, Z - 1u))));
+                wv[j] = voxel_word_nc(w, (uint32_t)jx, (uint32_t)jy, (uint32_t)jz);   // unused outside
                 if (j == G - 1 && chk) {   // after the last voxel gather: all G + 1 loads in flight
                     const uint32_t cx = (uint32_t)imin(imax(jx >> 1, 0), w.SX - 1);
                     const uint32_t cy = (uint32_t)imin(imax(jy >> 1, 0), w.SY - 1);
@@ -621,7 +694,8 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                     cw = csdf_word_at(w, cx, cy, cz);
                     ccx = cx;
                 }
-                bm[j] = ob ? 0u : (1u << voxel_bit(w, (uint32_t)jx, (uint32_t)jy));   // 0: outside
+                obv[j] = ob;
+                sh[j] = voxel_shift(w, (uint32_t)jx, (uint32_t)jy);
                 const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
                 const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
                 ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
@@ -633,7 +707,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             const bool jp = jd1 > 2;
 #pragma unroll
             for (int j = G - 1; j >= 0; j--) {
-                bool stop = ((wv[j] & bm[j]) != 0u) | (bm[j] == 0u);
+                bool stop = (((wv[j] >> (sh[j] & 31u)) & 1u) != 0u) | obv[j];
                 if (j == G - 1) stop = stop | jp;
                 k = stop ? j : k;
             }
@@ -747,16 +821,17 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 st = jd > 2 ? 1 : 0;
             }
             const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
-            // clamped (always valid) gather; its bit only counts in bounds
-            const uint32_t qx = umin((uint32_t)ix, X - 1u), qy = umin((uint32_t)iy, Y - 1u), qz = umin((uint32_t)iz, Z - 1u);
+            // always-valid gather; its bit only counts in bounds
             uint32_t word;
             if (REUSE) {   // a word covers 8 (x) x 4 (y) voxels: runs along x/y re-read it
+                const uint32_t qx = umin((uint32_t)ix, X - 1u), qy = umin((uint32_t)iy, Y - 1u), qz = umin((uint32_t)iz, Z - 1u);
                 const uint32_t off = voxel_word_off(w, qx, qy, qz);
                 if (off != v_off) { v_word = voxel_load(w, off); v_off = off; }
                 word = v_word;
             } else {
-                RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, qx, qy, qz)));
-                word = voxel_word_at(w, qx, qy, qz);
+                RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, umin((uint32_t)ix, X - 1u), umin((uint32_t)iy, Y - 1u),
+                                                           umin((uint32_t)iz, Z - 1u))));
+                word = voxel_word_nc(w, (uint32_t)ix, (uint32_t)iy, (uint32_t)iz);
             }
             const bool solid = (word >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
             if (COUNT) sc.dda += (st == 0) & !oob;

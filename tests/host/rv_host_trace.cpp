@@ -23,18 +23,19 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
     World& w = h.w;
     w.X = 1 << lx; w.Y = 1 << ly; w.Z = 1 << lz;
     w.lbx = lx - 3; w.lbxy = (lx - 3) + (ly - 3);
+    w.lbz = lz - 3; w.lbzy = (lz - 3) + (ly - 3);
     w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
     w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
     const uint64_t nbricks = ((uint64_t)w.X * w.Y * w.Z) / 512;
-    w.coff = csdf_region(nbricks);
+    world_set_regions(w, nbricks);
     h.brick.assign((size_t)(((uint64_t)w.X * w.Y * w.Z) / 16), 0u);   // 128 B per brick
     for (uint64_t z = 0; z < (uint64_t)w.Z; z++)
         for (uint64_t y = 0; y < (uint64_t)w.Y; y++)
             for (uint64_t x = 0; x < (uint64_t)w.X; x++) {
                 uint64_t ci = x | (y << lx) | (z << (lx + ly));
                 if (!((bits[ci >> 5] >> (ci & 31)) & 1u)) continue;
-                uint64_t b = (x >> 3) | ((y >> 3) << w.lbx) | ((z >> 3) << w.lbxy);
+                uint64_t b = brick_of(w, x >> 3, y >> 3, z >> 3);
                 uint32_t bit = (uint32_t)((x & 7) | ((y & 7) << 3) | ((z & 7) << 6));
                 h.brick[bits_word_index(b, bit >> 5)] |= 1u << (bit & 31);
             }
@@ -42,7 +43,7 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
     for (uint64_t cz = 0; cz < (uint64_t)w.SZ; cz++)
         for (uint64_t cy = 0; cy < (uint64_t)w.SY; cy++)
             for (uint64_t cx = 0; cx < (uint64_t)w.SX; cx++) {
-                uint64_t b = (cx >> 2) | ((cy >> 2) << w.lbx) | ((cz >> 2) << w.lbxy);
+                uint64_t b = brick_of(w, cx >> 2, cy >> 2, cz >> 2);
                 uint32_t local = (uint32_t)((cx & 3) | ((cy & 3) << 2) | ((cz & 3) << 4));
                 bytes[csdf_byte_index(w.coff, b, local)] = csdf[(cz * w.SY + cy) * w.SX + cx];
             }
