@@ -322,6 +322,18 @@ RV_HD uint32_t voxel_word_at(const WV& w, uint32_t x, uint32_t y, uint32_t z) {
     return voxel_load(w, voxel_word_off(w, x, y, z));
 }
 
+// Bit (shift & 31) of a word: v_bfe_u32 reads only the offset's low 5 bits, so voxel_shift
+// needs no mask.
+RV_HD uint32_t word_bit(uint32_t word, uint32_t shift) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ubfe(word, shift, 1u);
+#else
+    return (word >> (shift & 31u)) & 1u;
+#endif
+}
+// index of the lowest set bit of a non-zero word (v_ffbl_b32)
+RV_HD uint32_t lowest_bit(uint32_t v) { return (uint32_t)__builtin_ctz(v); }
+
 // (int)floorf(x) in one instruction on gfx950 (v_cvt_flr_i32_f32; the compiler only forms it
 // under no-NaN fast math).  Equal to floor + convert for every non-NaN input, denormals included.
 RV_HD int floor_i(float x) {
@@ -664,10 +676,12 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         uint32_t jd = 0;
         if constexpr (G > 1 && RW) {
         // Look-ahead, stop search + re-walk.  The walk of a group visits the G cells the DDA would
-        // visit if it did not stop (data-independent), gathers their words and, per cell, its bit's
-        // shift and whether it lies outside the grid.  The stop search is then a bit extract, a
-        // compare and a select per step: the first cell whose bit is set or that lies outside, or
-        // the group's check.
+        // visit if it did not stop (data-independent) and gathers their words.  The stop search is
+        // a G-bit mask -- bit j: cell j's voxel is solid, bit G - 1 also: the group's check jumps,
+        // bit G: no stop -- whose lowest set bit is the stopping step.  Bounds: each coordinate
+        // moves one way, so a group whose first and last cells are inside the grid lies inside;
+        // only a group that leaves (or starts outside, after an exhausted sphere march) walks its
+        // cells again for their bounds.
         // Only where a lane stops are its k < G steps walked again from the group start, so the
         // per-step selection and state updates run once per step instead of twice.
         static_assert(G == 2 || G == 4 || G == 8, "the look-ahead group divides 8");
@@ -675,14 +689,15 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         bool jmp = false;
         for (int i0 = 0; i0 < 200; i0 += G) {
             uint32_t wv[G], sh[G];
-            bool obv[G];
             uint32_t cw = 0, ccx = 0;
             const bool chk = ((i0 + G - 1) & 7) == 7;   // wave-uniform
             int jx = ix, jy = iy, jz = iz, jm = mask;
             float ux = tx, uy = ty, uz = tz;
+            bool ob_ends = false;   // first or last cell outside
 #pragma unroll
             for (int j = 0; j < G; j++) {
-                const bool ob = ((uint32_t)jx >= X) | ((uint32_t)jy >= Y) | ((uint32_t)jz >= Z);
+                if (j == 0 || j == G - 1)
+                    ob_ends = ob_ends | ((uint32_t)jx >= X) | ((uint32_t)jy >= Y) | ((uint32_t)jz >= Z);
                 RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, umin((uint32_t)jx, X - 1u), umin((uint32_t)jy, Y - 1u),
                                                            umin((uint32_t)jz, Z - 1u))));
                 wv[j] = voxel_word_nc(w, (uint32_t)jx, (uint32_t)jy, (uint32_t)jz);   // unused outside
@@ -694,7 +709,6 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                     cw = csdf_word_at(w, cx, cy, cz);
                     ccx = cx;
                 }
-                obv[j] = ob;
                 sh[j] = voxel_shift(w, (uint32_t)jx, (uint32_t)jy);
                 const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
                 const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
@@ -702,15 +716,25 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 jx += selx ? sx : 0; jy += sely ? sy : 0; jz += selz ? sz : 0;
                 if (j == G - 1) jm = selx ? 0 : (sely ? 1 : 2);
             }
-            int k = G;
             const uint32_t jd1 = csdf_byte(cw, ccx);   // 0 in a group without a check
             const bool jp = jd1 > 2;
+            uint32_t sm = (1u << G) | (jp ? 1u << (G - 1) : 0u);
 #pragma unroll
-            for (int j = G - 1; j >= 0; j--) {
-                bool stop = (((wv[j] >> (sh[j] & 31u)) & 1u) != 0u) | obv[j];
-                if (j == G - 1) stop = stop | jp;
-                k = stop ? j : k;
+            for (int j = 0; j < G; j++) sm |= word_bit(wv[j], sh[j]) << j;
+            if (ob_ends) {   // the cells outside the grid stop the walk too
+                int qx = ix, qy = iy, qz = iz;
+                float vx = tx, vy = ty, vz = tz;
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    const bool ob = ((uint32_t)qx >= X) | ((uint32_t)qy >= Y) | ((uint32_t)qz >= Z);
+                    sm |= ob ? 1u << j : 0u;
+                    const bool cxy = vx < vy, cxz = vx < vz, cyz = vy < vz;
+                    const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
+                    vx = selx ? vx + ddx : vx; vy = sely ? vy + ddy : vy; vz = selz ? vz + ddz : vz;
+                    qx += selx ? sx : 0; qy += sely ? sy : 0; qz += selz ? sz : 0;
+                }
             }
+            const int k = (int)lowest_bit(sm);
             if (k < G) {
                 kk = k;
                 jmp = jp & (k == G - 1);
@@ -833,7 +857,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                                                            umin((uint32_t)iz, Z - 1u))));
                 word = voxel_word_nc(w, (uint32_t)ix, (uint32_t)iy, (uint32_t)iz);
             }
-            const bool solid = (word >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
+            const bool solid = word_bit(word, voxel_shift(w, (uint32_t)ix, (uint32_t)iy)) != 0u;
             if (COUNT) sc.dda += (st == 0) & !oob;
             st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
             const bool go = st == 0;

@@ -22,6 +22,8 @@ for step in "$@"; do
                rc=$?; [ $rc -le 1 ] || exit 3 ;;
         bench) run bench 600 python bench.py || exit 3 ;;
         bench_c3) run bench_c3 600 python bench.py --config c3 --cpu-seconds 5 || exit 3 ;;
+        bench_c2) run bench_c2 600 python bench.py --config c2 --cpu-seconds 5 || exit 3 ;;
+        bench_c1) run bench_c1 600 python bench.py --config c1 --cpu-seconds 5 || exit 3 ;;
         bench_c5) run bench_c5 600 python bench.py --config c5 --cpu-seconds 0 --steps 128 || exit 3 ;;
         bench_c4) run bench_c4 600 python bench.py --config c4 --cpu-seconds 0 --steps 128 || exit 3 ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
