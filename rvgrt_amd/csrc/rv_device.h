@@ -972,9 +972,11 @@ RV_HD f3 cone_dir(int k, f3 up, f3 right, f3 fwd) {
 }
 // CB = cones per group whose first-step gathers go out together (1: each
 // cone's CSDF byte and GI texel at once, 6 round trips instead of 12; 2, 3, 6:
-// fewer round trips for more live registers).
+// fewer round trips for more live registers).  6 since the round-2 traversal diet left the
+// pipelined launch register room at 8 waves/SIMD (56 -> 64 VGPRs): k_ref_pipe C4 -2 %, C3 -2 %
+// against 1 (profiles/r02/cone_group_ab.txt; at 72 VGPRs in round 1 it cost a wave and 5 %).
 #ifndef RV_CONE_GROUP
-#define RV_CONE_GROUP 1
+#define RV_CONE_GROUP 6
 #endif
 template <bool COUNT, int CB = RV_CONE_GROUP, class WV = World>
 RV_HD f3 trace_cones6(const WV& w, f3 pos, f3 up, f3 right, f3 fwd, uint32_t& steps) {
