@@ -285,7 +285,7 @@ RV_HD uint32_t voxel_load(const LinearWorld& w, uint32_t off) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.bits) + off);
 }
 RV_HD uint32_t voxel_bit(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
-RV_HD uint32_t voxel_shift(const LinearWorld&, uint32_t x, uint32_t) { return x; }
+RV_HD uint32_t voxel_shift(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
 RV_HD uint32_t gi_texel(const LinearWorld& w, uint32_t idx) { return w.gi[idx]; }
 // GI grid (X/4 x Y/4 x Z/4, x fastest, power-of-two dims < 2^32 cells): log2 GX, log2 (GX * GY)
 RV_HD uint32_t gi_shift_x(const World& w) { return (uint32_t)w.lbx + 1u; }
@@ -688,7 +688,10 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         int kk = G;           // stop step inside the stopping group (G: no stop)
         bool jmp = false;
         for (int i0 = 0; i0 < 200; i0 += G) {
-            uint32_t wv[G], sh[G];
+            // bit shifts of the cells; G = 8 packs two per register (16-bit halves: a shift is
+            // < 2^14 for an in-range cell, and a cell after one outside the grid is never tested)
+            constexpr bool PK = G == 8;
+            uint32_t wv[G], sh[PK ? G / 2 : G];
             uint32_t cw = 0, ccx = 0;
             const bool chk = ((i0 + G - 1) & 7) == 7;   // wave-uniform
             int jx = ix, jy = iy, jz = iz, jm = mask;
@@ -709,7 +712,9 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                     cw = csdf_word_at(w, cx, cy, cz);
                     ccx = cx;
                 }
-                sh[j] = voxel_shift(w, (uint32_t)jx, (uint32_t)jy);
+                if (!PK) sh[j] = voxel_shift(w, (uint32_t)jx, (uint32_t)jy);
+                else if (j % 2 == 0) sh[j / 2] = voxel_shift(w, (uint32_t)jx, (uint32_t)jy);
+                else sh[j / 2] |= voxel_shift(w, (uint32_t)jx, (uint32_t)jy) << 16;
                 const bool cxy = ux < uy, cxz = ux < uz, cyz = uy < uz;
                 const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
                 ux = selx ? ux + ddx : ux; uy = sely ? uy + ddy : uy; uz = selz ? uz + ddz : uz;
@@ -720,7 +725,8 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
             const bool jp = jd1 > 2;
             uint32_t sm = (1u << G) | (jp ? 1u << (G - 1) : 0u);
 #pragma unroll
-            for (int j = 0; j < G; j++) sm |= word_bit(wv[j], sh[j]) << j;
+            for (int j = 0; j < G; j++)
+                sm |= word_bit(wv[j], !PK ? sh[j] : (j % 2 == 0 ? sh[j / 2] : sh[j / 2] >> 16)) << j;
             if (ob_ends) {   // the cells outside the grid stop the walk too
                 int qx = ix, qy = iy, qz = iz;
                 float vx = tx, vy = ty, vz = tz;
