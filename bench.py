@@ -88,9 +88,10 @@ def main():
                          "static: one camera for every frame (round 1)")
     ap.add_argument("--pan", type=float, default=0.0005, help="yaw change per frame of the camera path (rad)")
     ap.add_argument("--tile-px", type=int, default=None,
-                    help="screen-tile size of the N>1 shard (default: 16 px without the pre-pass, 32 with it; "
+                    help="screen-tile size of the N>1 shard (default: 16 px without the pre-pass, 64 with it; "
                          "tools/shard_probe.py: C2 at 8 ranks renders its slowest share in 19.6 us/frame at "
-                         "16 px vs 30.9 at 64 px)")
+                         "16 px vs 30.9 at 64 px; the pipelined C4 share at 2/4/8 ranks in 288/181/162 us at "
+                         "64 px vs 303/194/168 at 32, the half-res halo costing less)")
     ap.add_argument("--root-weight", type=float, default=None,
                     help="N>1 native loop: rank 0's share of tiles relative to the others (rank 0 also receives "
                          "and assembles every frame); default 1 - 0.019 (N-1): its measured assembly cost is "
@@ -247,7 +248,7 @@ def main():
                              + 20 * gi_stats["tex_samples"] + 8 * gi_cells)
 
     # ---------------------------------------------------------------- tiles
-    T = args.tile_px if args.tile_px else (32 if prepass else 16)
+    T = args.tile_px if args.tile_px else (64 if prepass else 16)
     tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
     ntiles = tiles_x * tiles_y
     my_tiles = np.arange(rank, ntiles, world_size, dtype=np.int32)

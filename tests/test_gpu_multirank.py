@@ -57,6 +57,7 @@ def _run_ranks(fns):
 @pytest.mark.parametrize("flags,T,N,w0,bpp", [
     (8, 16, 2, 1.0, 3), (8, 16, 3, 0.9, 4), (8, 32, 8, 0.87, 3),       # batched groups (C1/C2 loop)
     (7, 32, 2, 1.0, 3), (7, 32, 3, 0.94, 4), (7, 16, 8, 0.87, 3),      # pipelined reference frames (C3-C5 loop)
+    (7, 64, 2, 0.98, 3), (7, 64, 4, 0.94, 4),                         # the bench's reference-frame tile size
 ])
 def test_loopback_ranks_equal_one_context(rv, atlas, flags, T, N, w0, bpp):
     from rvgrt_amd.configs import TEST_POSES_128, camera_path
