@@ -592,6 +592,9 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 // Build-time defaults of the traversal variants (kernels pick per launch
 // shape, see rv_kernels.hip): G = DDA look-ahead group, REUSE = keep the last
 // gathered word of each phase and gather again only when its address moves.
+#ifndef RV_PACK_SHIFTS   // G = 8 groups keep their cells' bit shifts two per VGPR
+#define RV_PACK_SHIFTS 1
+#endif
 #ifndef RV_DDA_REWALK    // look-ahead groups: stop search + re-walk of the stopping group (G > 1)
 #define RV_DDA_REWALK 1
 #endif
@@ -690,7 +693,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         for (int i0 = 0; i0 < 200; i0 += G) {
             // bit shifts of the cells; G = 8 packs two per register (16-bit halves: a shift is
             // < 2^14 for an in-range cell, and a cell after one outside the grid is never tested)
-            constexpr bool PK = G == 8;
+            constexpr bool PK = G == 8 && RV_PACK_SHIFTS;
             uint32_t wv[G], sh[PK ? G / 2 : G];
             uint32_t cw = 0, ccx = 0;
             const bool chk = ((i0 + G - 1) & 7) == 7;   // wave-uniform
