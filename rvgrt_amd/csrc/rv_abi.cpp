@@ -780,6 +780,7 @@ static FrameParams make_params(rv_ctx* c, const rv_camera* cam, const float* vp,
     f.up = host_v(cam->up[0], cam->up[1], cam->up[2]);
     f.sun = sun_dir();
     f.time = time; f.jx = jx; f.jy = jy;
+    cone_basis_scales(f.cone_k1, f.cone_k2);
     for (int i = 0; i < 16; i++) {
         f.vp[i] = vp ? vp[i] : (i % 5 == 0 ? 1.0f : 0.0f);
         f.pvp[i] = pvp ? pvp[i] : f.vp[i];

@@ -1053,6 +1053,22 @@ RV_HD f3 trace_cones6(const WV& w, f3 pos, f3 up, f3 right, f3 fwd, uint32_t& st
     return total;
 }
 
+// computeColor's cone basis (src/StateRender.cu:110-112): right = normalize(cross(n, c)),
+// fwd = normalize(cross(n, right)), c = (0.577, 0.577, 0.577).  For an axis normal n (every
+// defined hit: +-1 on one axis, +0 elsewhere) cross(n, c) has two components of magnitude 0.577
+// and a zero, so its length is sqrt(a + a), a = 0.577 * 0.577, for all six normals; likewise
+// cross(n, right) has two of magnitude r = 0.577 * k1 and a zero.  The two normalizations' scale
+// factors 1 / length are therefore frame constants (host-computed with the same correctly
+// rounded sqrt and division; normalize(v) = v * (1 / |v|) component-wise, so the products are
+// identical).  A zero normal (an undefined hit) keeps the generic path.
+RV_HD void cone_basis_scales(float& k1, float& k2) {
+    const float a = 0.577f * 0.577f;
+    k1 = 1.0f / sqrtf(a + a);
+    const float r = 0.577f * k1;
+    const float b = r * r;
+    k2 = 1.0f / sqrtf(b + b);
+}
+
 // sampleSky (src/raytracing_functions.cu:10-26)
 RV_HD f3 sample_sky(f3 dir, f3 sun) {
     if (dot(dir, sun) > 0.999f) return V(1.0f * 10.0f, 0.9f * 10.0f, 0.2f * 10.0f);

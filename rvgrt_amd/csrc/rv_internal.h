@@ -43,6 +43,7 @@ enum : uint32_t { HI_HIT = 1u, HI_UNDEF = 2u, HI_WATER = 4u, HI_SHADOWED = 8u, H
 struct FrameCam {
     f3 pos, fo, ri, up;
     float time, jx, jy;
+    float cone_k1, cone_k2;  // cone_basis_scales(): 1/|cross(n, c)|, 1/|cross(n, right)| for an axis normal n
     float vp[16], pvp[16];
 };
 
@@ -52,6 +53,7 @@ struct FrameParams {
     uint32_t* chunk_cost[2];     // SCHED_COST: this frame's max wave lifetime per chunk (10 ns ticks)
     f3 pos, fo, ri, up, sun;
     float time, jx, jy;
+    float cone_k1, cone_k2;  // cone_basis_scales(): 1/|cross(n, c)|, 1/|cross(n, right)| for an axis normal n
     float vp[16], pvp[16];
     int W, H, hw, hh, flags;
     uint32_t* color; size_t color_pitch;
