@@ -95,18 +95,31 @@ def check_world_rays_gi(r, rv, oracle, atlas, log2, seed, gi_window=True):
     return ow
 
 
-def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=6):
+def spread_rows(H, n, rng):
+    """n rows spread evenly over the frame (jittered inside their bands), plus
+    the first, middle and last rows."""
+    band = H / n
+    rows = (np.arange(n) * band + rng.uniform(0, band, n)).astype(int)
+    return sorted(set(np.clip(rows, 0, H - 1).tolist()) | {0, H // 2, H - 1})
+
+
+def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=64):
+    """Sampled rows of the GPU frame against the oracle: RGBA8, MV and depth
+    bit-exact (the HIP path computes the oracle's arithmetic: no contraction,
+    correctly rounded division/sqrt; ocml's powf has matched glibc's on every
+    pixel so far).  The tolerance of SURVEY s8c is for the reference's own
+    compiled arithmetic, priced separately (tests/test_r9_numerics.py)."""
     img = r.readback(rv.RV_IMAGE_COLOR)
     mv = r.readback(rv.RV_IMAGE_MOTION)
     dep = r.readback(rv.RV_IMAGE_DEPTH)
     fr = oracle.make_frame(W, H, flags, cam_d, time=time)
-    rows = sorted(set(rng.integers(0, H, nrows).tolist()) | {0, H // 2, H - 1})
+    rows = spread_rows(H, nrows, rng)
     ref = oracle.render_rows(ow, fr, rows, want_stats=False)
     d = np.abs(img[rows].astype(np.int32) - ref["rgba"][rows].astype(np.int32)).max(axis=-1)
-    print(f"rows {rows}: {int((d > 0).sum())} of {d.size} pixels differ, max |d| {int(d.max())}")
-    assert d.max() <= 2 and (d == 0).mean() >= 0.995                       # the frame tolerance (powf ulps)
+    print(f"{len(rows)} rows: {int((d > 0).sum())} of {d.size} pixels differ, max |d| {int(d.max())}")
+    assert d.max() == 0
     assert np.array_equal(mv[rows], ref["mv"][rows]) and np.array_equal(dep[rows], ref["depth"][rows])
-    return rows
+    return rows, ref
 
 
 def test_c1_full_world_full_frame(rv, atlas, oracle):
@@ -127,8 +140,7 @@ def test_c1_full_world_full_frame(rv, atlas, oracle):
         r.frame(cam, vp, flags=cfg.flags | rv.RV_F_STATS)
         img = r.readback(rv.RV_IMAGE_COLOR)
         ref = oracle.render(ow, oracle.make_frame(W, H, cfg.flags, rv.camera_dict(cam, vp)))
-        d = np.abs(img.astype(np.int32) - ref["rgba"].astype(np.int32)).max(axis=2)
-        assert d.max() <= 2 and (d == 0).mean() >= 0.995, pose
+        assert np.array_equal(img, ref["rgba"]), pose
         assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"])
         assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"])
         st = r.stats()
@@ -137,7 +149,8 @@ def test_c1_full_world_full_frame(rv, atlas, oracle):
     r.close()
 
 
-@pytest.mark.parametrize("cfgname,pose", [("c2", "P0"), ("c3", "P0"), ("c3", "P1"), ("c4", "P0"), ("c5", "P0")])
+@pytest.mark.parametrize("cfgname,pose", [("c2", "P0"), ("c3", "P0"), ("c3", "P1"), ("c4", "P0"), ("c4", "P1"),
+                                         ("c5", "P0"), ("c5", "P1")])
 def test_fullsize_world_traversal_gi_frame_rows(rv, atlas, oracle, cfgname, pose):
     from rvgrt_amd.configs import CONFIGS, pose_f32
     cfg = CONFIGS[cfgname]
@@ -175,9 +188,18 @@ def test_reference_native_config_draw_cuda(rv, atlas, oracle):
     cam, vp = rv.camera_from_pose((128.0, 350.0, 128.0), f32(-0.7), f32(-math.pi - 0.3), W, H)
     d = rv.camera_dict(cam, vp)
     r.draw_cuda(d["pos"], d["fo"], d["up"], d["ri"], vp, vp, 0.3, 0.7)   # jitterX ignored, time = 0.7
-    rows = check_rows(r, rv, oracle, ow, W, H, flags | rv.RV_F_REF_FETCH, d, np.random.default_rng(7), time=0.7,
-                      nrows=8)
-    assert len(rows) >= 8
+    rows, ref = check_rows(r, rv, oracle, ow, W, H, flags | rv.RV_F_REF_FETCH, d, np.random.default_rng(7),
+                           time=0.7)
+    assert len(rows) >= 64
+    # R9 on the reference's own configuration: the same rows with the arithmetic
+    # nvcc compiles the reference to (FMA contraction, oracle/r9_study.py) stay
+    # within the SURVEY s8c tolerance of the uncontracted ones
+    with oracle.numerics("fma_gcc"):
+        var = oracle.render_rows(ow, oracle.make_frame(W, H, flags | rv.RV_F_REF_FETCH, d, time=0.7), rows,
+                                 want_stats=False)
+    dv = np.abs(var["rgba"][rows].astype(np.int32) - ref["rgba"][rows].astype(np.int32)).max(axis=-1)
+    print(f"native rows under FMA contraction: {(dv == 0).mean():.5f} exact, {(dv <= 2).mean():.5f} within 2 LSB")
+    assert (dv <= 2).mean() >= 0.995
     # how much the R6 fetch matters on this frame: the same rows with exact texel indices (informational)
     fr = oracle.make_frame(W, H, flags, d, time=0.7)
     img = r.readback(rv.RV_IMAGE_COLOR)

@@ -2,9 +2,11 @@
 
 Bar: bit-exact for the integer/byte world data (bits, CSDF, GI) and for the
 traversal (hit flag, voxel, position, normal, uv, step counts) -- both sides
-use separately rounded IEEE float ops.  Frames: RGBA8 |d| <= 2 LSB on every
-pixel and >= 99.5 % pixels exact (tolerance absorbs powf ulp differences in
-the fog / Fresnel terms).
+use separately rounded IEEE float ops.  Frames: RGBA8, MV and depth
+bit-exact as well (ocml's powf has matched glibc's on every pixel so far).
+The SURVEY.md s8c tolerance (|d| <= 2 LSB on >= 99.5 % of pixels) is kept
+for the reference's own compiled arithmetic -- FMA contraction, CUDA's
+tanf/powf -- and priced in tests/test_r9_numerics.py.
 """
 import numpy as np
 import pytest
@@ -119,8 +121,7 @@ def test_frame_parity(rv, atlas, oracle_world, oracle, name, flags, pose):
     st = r.stats()
     ref = oracle.render(ow, oracle.make_frame(W, H, flags, ocam))
     diff = np.abs(gpu.astype(np.int32) - ref["rgba"].astype(np.int32)).max(axis=2)
-    assert diff.max() <= 2, f"max |d| = {diff.max()}"
-    assert (diff == 0).mean() >= 0.995
+    assert diff.max() == 0, f"{int((diff > 0).sum())} pixels differ, max |d| = {diff.max()}"
     assert np.array_equal(gdep, ref["depth"])
     assert np.array_equal(gmv, ref["mv"])
     if flags & 1:
@@ -244,9 +245,8 @@ def test_golden_fixtures(rv, atlas):
 def test_golden_frames(rv, atlas):
     """The six golden frames of tests/golden (160x96 on the 128^3 world, C1 /
     C2 / reference flags, poses P0 / P1): MV and depth hashes and the work
-    counters equal the fixture exactly; RGBA8 equals the fixture PNG within
-    the frame tolerance (|d| <= 2 LSB, >= 99.5 % exact; hash equality
-    reported)."""
+    counters equal the fixture exactly; RGBA8 hashes equal the fixture's (the
+    decoded PNG is compared first for a readable failure)."""
     import hashlib
     import json
     import os
@@ -273,9 +273,10 @@ def test_golden_frames(rv, atlas):
         with open(os.path.join(gdir, f"{key}.png"), "rb") as f:
             want = decode_png(f.read())
         d = np.abs(img.astype(np.int32) - want.astype(np.int32)).max(axis=2)
-        assert d.max() <= 2 and (d == 0).mean() >= 0.995, key
-        exact += sha(img) == fr["rgba"]
-    print(f"golden frames with identical RGBA8 hash: {exact}/{len(g['frames'])}")
+        assert d.max() == 0, (key, int((d > 0).sum()), int(d.max()))
+        assert sha(img) == fr["rgba"], key
+        exact += 1
+    assert exact == len(g["frames"]) == 6
     r.close()
 
 
@@ -467,8 +468,7 @@ def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order, rays)
         off = 0 if off + rays >= ngi else off + rays
     assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi)
     ref_img = oracle.render(ow, oracle.make_frame(W, H, flags, rv.camera_dict(cam, vp)))["rgba"]
-    d = np.abs(r.readback(rv.RV_IMAGE_COLOR).astype(np.int32) - ref_img.astype(np.int32))
-    assert d.max() <= 2 and (d.max(axis=2) == 0).mean() >= 0.995
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref_img)
     assert np.array_equal(r.readback(rv.RV_IMAGE_HALF_DIST), ref.readback(rv.RV_IMAGE_HALF_DIST))
     r.close()
     ref.close()
