@@ -77,8 +77,11 @@ def camera_path(pose, width, height, frames, start=0, pan=0.0005, ref_compat=Tru
     for a camera panning `pan` rad of yaw per frame from `pose` ((pos, yaw,
     pitch) as RenderConfig.pose returns it): frame f's camera and unjittered
     VP from Character::Update, the previous frame's VP, and the jitter
-    sequence -- mapped as drawCUDA maps it with ref_compat (time <- jitterY,
-    jitter <- (0, 0)), or applied as ray jitter without.
+    sequence -- with ref_compat, time and jitter mapped as drawCUDA maps them
+    (time <- jitterY, jitter <- (0, 0)), or applied as
+    ray jitter without.  (The other ref_compat quirk, minDist's texel fetch
+    RV_F_REF_FETCH, belongs to the context: rv_draw_cuda and
+    rv_render_frame_seq both add it on a context created with ref_compat.)
     Returns frames + 1 rv_frame_desc: frames start..start+frames-1 and the
     one after them (rv_render_frame_seq's `next`)."""
     import numpy as np

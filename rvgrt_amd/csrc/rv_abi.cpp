@@ -2210,7 +2210,8 @@ rv_status rv_tile_shard_assign(int32_t width, int32_t height, int32_t tile_px, i
 rv_status rv_set_tile_shard_weighted(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks, float root_weight) {
     if (!c || nranks < 0 || (nranks > 0 && (rank < 0 || rank >= nranks))) return RV_ERR_INVALID;
     if (nranks > 0 && (tile_px < 16 || (tile_px & 15))) return fail(c, RV_ERR_INVALID, "tile_px must be a multiple of 16");
-    if (!(root_weight > 0.0f && root_weight <= 1.0f)) return fail(c, RV_ERR_INVALID, "root weight must be in (0, 1]");
+    if (nranks > 0 && !(root_weight > 0.0f && root_weight <= 1.0f))   // turning sharding off takes any weight
+        return fail(c, RV_ERR_INVALID, "root weight must be in (0, 1]");
     c->shard_n = nranks; c->shard_rank = rank; c->shard_px = tile_px; c->shard_w0 = root_weight;
     c->shard_ids.clear(); c->shard_all.clear(); c->shard_max = 0;
     if (nranks == 0) return RV_OK;
@@ -2250,7 +2251,12 @@ rv_status rv_set_gather_bpp(rv_ctx* c, int32_t bpp) {
 // The ranks of a communicator must agree on everything that shapes the
 // exchange (shard, deal weight, packing, frame size, GI window), or the
 // slices and all-gathers would mismatch: checked with one all-gather of a
-// hash when the configuration changes (then a bounded host wait).
+// hash at the start of EVERY rv_render_frame_seq / rv_render_frames call
+// with a communicator (then a bounded host wait).  The exchange is
+// unconditional so every rank issues the same collectives in the same
+// order: a rank whose configuration changed after an agreed call and a rank
+// whose did not both enter it, see the disagreement and return
+// RV_ERR_INVALID before any tile or GI exchange is issued.
 static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint64_t v) { for (int b = 0; b < 8; b++) { h ^= (v >> (8 * b)) & 255u; h *= 1099511628211ull; } };
@@ -2260,7 +2266,6 @@ static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
     mix(w0); mix((uint64_t)c->shard_max); mix((uint64_t)c->cfg.width); mix((uint64_t)c->cfg.height);
     mix((uint64_t)c->cfg.gi_rays_per_frame); mix((uint64_t)(flags & ~RV_F_STATS));
     for (int32_t t : c->shard_all) mix((uint64_t)(uint32_t)t);
-    if (comm->verified == h) return RV_OK;
     if (!c->comm_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     uint64_t* d = nullptr;
     HIP_TRY(c, hipMalloc(&d, 8 * (size_t)(comm->nranks + 1)));
@@ -2284,7 +2289,11 @@ static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
 
 static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
     const int frames = q.n;
+    if (c->cfg.ref_compat) flags |= RV_F_REF_FETCH;   // as rv_draw_cuda: the minDist fetch of a ref_compat context
     if (comm) {
+        // a communicator belongs to the context it was created on (rv_comm_destroy
+        // detaches only that one, rv_sync / rv_destroy wait on it)
+        if (comm->ctx != c) return fail(c, RV_ERR_INVALID, "communicator was created on another context");
         c->comm_attached = comm;
         if (rv_status vs = verify_ranks(c, comm, flags)) return vs;
     }

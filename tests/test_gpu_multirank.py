@@ -131,6 +131,49 @@ def test_loopback_rank_disagreement_is_rejected(rv, atlas):
     group.close()
 
 
+def test_loopback_disagreement_after_agreed_call_is_rejected(rv, atlas):
+    """An agreed first call, then rank 1 alone changes its deal weight: the
+    next call fails on both ranks (the configuration exchange runs on every
+    call, so both enter it) instead of desynchronising the collectives."""
+    group = rv.LoopbackGroup(2, timeout_ms=30000)
+    rs = [_make(rv, atlas, 8) for _ in range(2)]
+    comms = []
+    for q, r in enumerate(rs):
+        r.set_tile_shard(16, q, 2, root_weight=1.0)
+        comms.append(rv.Comm.loopback(r, group, q))
+    from rvgrt_amd.configs import TEST_POSES_128
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
+    _run_ranks([lambda q=q: rs[q].render_frames(2, cam, vp, comm=comms[q]) for q in range(2)])
+    for c in comms:
+        c.wait(60000)
+    rs[1].set_tile_shard(16, 1, 2, root_weight=0.8)
+    errs = []
+
+    def body(q):
+        try:
+            rs[q].render_frames(2, cam, vp, comm=comms[q])
+        except rv.RvError as e:
+            errs.append(str(e))
+    ts = [threading.Thread(target=body, args=(q,)) for q in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+        assert not t.is_alive(), "a rank thread hung"
+    assert len(errs) == 2 and all("disagree" in e for e in errs), errs
+    # a communicator used with a context other than its own is rejected
+    other = _make(rv, atlas, 8)
+    other.set_tile_shard(16, 0, 2)
+    with pytest.raises(rv.RvError, match="another context"):
+        other.render_frames(1, cam, vp, comm=comms[0])
+    other.close()
+    for c in comms:
+        c.close()
+    for r in rs:
+        r.close()
+    group.close()
+
+
 def test_loopback_missing_rank_times_out(rv, atlas):
     """A peer that never arrives: the loop call returns an error after the
     group's timeout (2 s here), and the communicator can still be closed."""
