@@ -109,6 +109,10 @@ def main():
     ap.add_argument("--pipe", type=int, default=1,
                     help="native loop, per-frame GI + pre-pass (C3-C5), one GPU: one k_ref_pipe launch per frame "
                          "runs render k | GI update k+1 | pre-pass k+1 (0: one frame at a time)")
+    ap.add_argument("--group", type=int, default=None,
+                    help="native loop, reference frames (C3-C5): frames per launch of the grouped loop "
+                         "(rv_set_frame_group; GI update split into traced records + a per-frame combine, "
+                         "phase A sharded over the ranks); 0 = the per-frame pipeline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collective backend; gloo (host-staged gather, ranks may share a GPU) "
                          "only rehearses the multi-rank path")
@@ -184,6 +188,8 @@ def main():
     streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.stream_priority) for _ in range(nfl - 1)]
     r.set_gi_async(args.gi_async)
     r.set_pipeline(args.pipe)
+    group = args.group if args.group is not None else 0
+    r.set_frame_group(group)
     t0 = time.perf_counter()
     r.world_build()
     for s in range(max(cfg.gi_sweeps, 0)):
@@ -199,6 +205,8 @@ def main():
     # pan of --pan rad per frame, and each frame's previous VP = the frame before's (motion vectors).
     # frames the run takes from the path: warm-up, timed, the stage-timing pass, 9 latency frames
     n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if nfl > 1 else min(args.steps, 10)
+    if group >= 2:   # whole groups: the timing pass records only full-group launches
+        n_stage_frames = group * max(2, min(args.steps // group, 6))
     n_path = args.warmup + args.steps + n_stage_frames + 9 + 2
     pan = args.pan if args.camera == "path" else 0.0
     path = camera_path((pos, yaw, pitch), W, H, n_path, pan=pan, ref_compat=args.camera == "path")
@@ -395,6 +403,10 @@ def main():
     piped = native and args.path == "fused" and args.pipe and gi_per_frame and bool(flags & rv.RV_F_PREPASS)
     gi_groups = grouped and gi_per_frame and bool(flags & rv.RV_F_PREPASS) and world_size == 1 and not piped
     fpl = nfl if (grouped and not gi_per_frame) else 1
+    # grouped reference frames: the effective group size (the library caps it by the GI grid)
+    ref_group = r.frame_group_effective() if piped and group >= 2 else 0
+    if ref_group >= 2:
+        fpl = ref_group
     stage_fpl = {name: fpl for name in rv._lib.STAGES}
     if gi_groups:
         stage_fpl["pp_primary"] = nfl
@@ -456,7 +468,8 @@ def main():
     dom = max((k for k in frame_stage_ms if k != "gi"), key=lambda k: frame_stage_ms[k])
     kernel_names = {"pp_primary": "k_prepass" if megakernel else "k_wf_pp_primary",
                     "pp_shadow": "k_wf_pp_shadow",
-                    "primary": ("k_ref_pipe" if piped else "k_render_tiles" if world_size > 1 else "k_render")
+                    "primary": ("k_ref_group" if ref_group else "k_ref_pipe" if piped else
+                                "k_render_tiles" if world_size > 1 else "k_render")
                     if megakernel else "k_wf_primary",
                     "shadow": "k_wf_shadow",
                     "water": "k_wf_water", "cones": "k_wf_cones", "shade": "k_wf_shade"}
@@ -464,7 +477,9 @@ def main():
     dom_fpl = stage_fpl[dom]
     dom_bytes = stage_bytes[dom] * dom_fpl
     if piped and dom == "primary":   # the launch also runs the next frame's pre-pass and GI update
-        dom_bytes = stage_bytes["primary"] + stage_bytes["pp_primary"] + stage_bytes.get("gi", 0)
+        # (grouped: the next group's pre-pass and phase A of the group after; phase B's combine is a
+        # separate small kernel, not counted here)
+        dom_bytes = (stage_bytes["primary"] + stage_bytes["pp_primary"] + stage_bytes.get("gi", 0)) * dom_fpl
     if world_size > 1:   # per-GPU: this rank's share of the stage's bytes
         dom_bytes = dom_bytes * len(my_tiles) / ntiles
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -481,7 +496,7 @@ def main():
     gathers = (g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]) * dom_fpl
     if piped and dom == "primary":
         for h in (st_stage["pp_primary"], gi_stats):
-            gathers += h["sphere_steps"] + h["dda_steps"] + h["csdf_checks"]
+            gathers += (h["sphere_steps"] + h["dda_steps"] + h["csdf_checks"]) * dom_fpl
     if world_size > 1:
         gathers = gathers * len(my_tiles) / ntiles
     gather_rate = gathers / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
@@ -533,6 +548,7 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},   # per launch
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
             "pipelined": bool(piped),
+            "frame_group": ref_group,
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,
             "root_weight": float(os.environ.get("RV_SHARD_ROOT_WEIGHT", "1")) if world_size > 1 and native else None,

@@ -77,6 +77,8 @@ SIGNATURES = [
     ("rv_tile_shard_assign", I32, [I32, I32, I32, I32, C.c_float, P]),
     ("rv_set_gi_async", I32, [P, I32]),
     ("rv_set_pipeline", I32, [P, I32]),
+    ("rv_set_frame_group", I32, [P, I32]),
+    ("rv_get_frame_group", I32, [P, C.POINTER(C.c_int32)]),
     ("rv_set_gi_stats", I32, [P, I32]),
     ("rv_set_frames_in_flight", I32, [P, I32]),
     ("rv_world_build", I32, [P]),
@@ -131,6 +133,8 @@ def load() -> C.CDLL:
                                "(make -C rvgrt_amd/csrc); there is no CPU fallback")
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            if os.environ.get("RVGRT_LIB") and not hasattr(L, name):
+                continue   # an older experiment build: entry points it predates stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

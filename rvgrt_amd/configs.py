@@ -79,9 +79,11 @@ def camera_path(pose, width, height, frames, start=0, pan=0.0005, ref_compat=Tru
     VP from Character::Update, the previous frame's VP, and the jitter
     sequence -- with ref_compat, time and jitter mapped as drawCUDA maps them
     (time <- jitterY, jitter <- (0, 0)), or applied as
-    ray jitter without.  (The other ref_compat quirk, minDist's texel fetch
-    RV_F_REF_FETCH, belongs to the context: rv_draw_cuda and
-    rv_render_frame_seq both add it on a context created with ref_compat.)
+    ray jitter without.  Only time and jitter are mapped here: the other
+    ref_compat quirk, minDist's normalized-coordinate texel fetch, is the frame
+    flag RV_F_REF_FETCH, which rv_draw_cuda adds on a ref_compat context and
+    a caller of rv_render_frame_seq / rv_frame passes in `flags` when it wants
+    it (the bench renders the exact texel fetch).
     Returns frames + 1 rv_frame_desc: frames start..start+frames-1 and the
     one after them (rv_render_frame_seq's `next`)."""
     import numpy as np

@@ -162,6 +162,15 @@ struct rv_ctx {
     uint64_t carry_chunk = 0; int carry_n = 0, carry_r = 0, carry_half = 0;
     float carry_key[24] = {};
     int pipe_carry = 1;            // RV_PIPE_CARRY
+    // grouped reference frames (rv_set_frame_group): frame sets per group parity, phase-A records
+    // (this rank's stage slots and the all-gathered ones, 3 groups each), the update ring, the
+    // phase-B stream and the loop's events
+    int group = 0;
+    BatchSet gsets[2];
+    uint2* grec_stage = nullptr; uint2* grec_all = nullptr; size_t grec_stage_n = 0, grec_all_n = 0;
+    uint32_t* gring = nullptr; size_t gring_n = 0;
+    hipStream_t grp_stream = nullptr;
+    hipEvent_t gev[8] = {};
     rv_comm* comm_attached = nullptr;   // the communicator of the last rv_render_frame_seq (bounded rv_sync)
     float shard_w0 = 1.0f;              // rank 0's tile weight of the shard (rv_set_tile_shard_weighted)
     // per-frame camera table of batched launches (rv_render_frame_seq): device copy, pinned staging
@@ -362,6 +371,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
+    if (const char* e = getenv("RV_GROUP")) c->group = std::min(16, std::max(0, atoi(e)));
     if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
         if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
         c->gather_bpp = atoi(e);
@@ -457,7 +467,11 @@ void rv_destroy(rv_ctx* c) {
     }
 #endif
     if (c->gi_stream) { hipStreamSynchronize(c->gi_stream); hipStreamDestroy(c->gi_stream); }
-    for (BatchSet& b : c->bsets) {
+    hipFree(c->grec_stage); hipFree(c->grec_all); hipFree(c->gring);
+    for (hipEvent_t e : c->gev) if (e) hipEventDestroy(e);
+    if (c->grp_stream) hipStreamDestroy(c->grp_stream);
+    for (BatchSet* bs : {&c->bsets[0], &c->bsets[1], &c->gsets[0], &c->gsets[1]}) {
+        BatchSet& b = *bs;
         hipFree(b.color); hipFree(b.mv); hipFree(b.depth); hipFree(b.hdist); hipFree(b.hshadow);
         hipFree(b.tbuf); hipFree(b.gbuf);
         if (b.rendered) hipEventDestroy(b.rendered);
@@ -589,6 +603,13 @@ rv_status rv_set_gi_async(rv_ctx* c, int32_t on) {
 rv_status rv_set_pipeline(rv_ctx* c, int32_t on) {
     if (!c) return RV_ERR_INVALID;
     c->pipe = on != 0;
+    c->carry_gi = c->carry_pp = false;
+    return RV_OK;
+}
+
+rv_status rv_set_frame_group(rv_ctx* c, int32_t n) {
+    if (!c || n < 0 || n > 16) return RV_ERR_INVALID;
+    c->group = n;
     c->carry_gi = c->carry_pp = false;
     return RV_OK;
 }
@@ -1980,6 +2001,321 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
     return RV_OK;
 }
 
+// Grouped reference frames (rv_set_frame_group; rvgrt.h).  Frames of the call in
+// groups of F; group g = frames [gF, gF + n_g).  On stream S:
+//   prologue  launch: pre-pass of group 0, phase A of groups 0 and 1; phase B of group 0
+//   launch g  render g (overlay: group g's updates) | pre-pass g+1 | phase A of group g+2
+//   then      apply(g): group g's updates from the ring into the grid (after render g, its last
+//             reader of the old cells; before render g+1)
+// Side stream SB: phase B of group g+2 once apply(g) and its records exist (the all-gather with a
+// communicator): it overlaps launch g+1; launch g+2 waits for it.  The ring holds the updates of
+// two consecutive groups at positions P (cumulative cell count, wrapping), so phase B of group h
+// reads grid h-1's cells through one overlay of origin (s_{h-1}, P_{h-1}), and every other cell
+// from the grid (complete through group h-2).  With a tile shard and a communicator the phase A
+// cells of every update are split over the ranks (rank r: the r-th chunk of each window) and the
+// records of a group all-gathered once; the packed tiles of group g go to rank 0 after launch g.
+static int group_frames(const rv_ctx* c) {
+    const uint64_t n = n_gi(c), rays = std::min<uint64_t>(c->cfg.gi_rays_per_frame, n);
+    int F = std::min(c->group, 16);
+    while (F >= 2 && (uint64_t)F * rays * 2 > n) F--;   // two groups' updates never overlap in the grid
+    return F >= 2 ? F : 0;
+}
+
+static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStream_t S, rv_comm* comm, int F) {
+    const int frames = q.n;
+    const int W = c->cfg.width, H = c->cfg.height;
+    const size_t hbytes = (size_t)(W / 2) * (H / 2) * 4;
+    const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
+    const int N = tiles ? c->shard_n : 1, R = tiles ? c->shard_rank : 0, T = c->shard_px;
+    const bool xchg = tiles && comm;
+    const bool probe = tiles && !comm && N > 1 && getenv("RV_GI_SHARD_PROBE") != nullptr;
+    const bool shard_gi = xchg || probe;
+    const int bpp = c->gather_bpp;
+    const size_t slice = tiles ? (size_t)c->shard_max * T * T * bpp : 0;
+    const uint64_t ngi = n_gi(c), rays = std::min<uint64_t>(c->cfg.gi_rays_per_frame, ngi);
+    const uint64_t chunk = shard_gi ? (rays + N - 1) / N : rays;   // phase-A cells per rank and window
+    const int Nrec = shard_gi ? N : 1;
+    uint64_t cap = 1;
+    while (cap < 2 * (uint64_t)F * rays) cap <<= 1;                  // the ring: two groups' updates
+    const uint32_t gmask = (uint32_t)(ngi - 1), cmask = (uint32_t)(cap - 1);
+    const int G = (frames + F - 1) / F;
+    auto nfr = [&](int g) { return g < G ? std::min(F, frames - g * F) : 0; };
+    // buffers
+    const size_t gneed = tiles && root ? slice * (size_t)F * (size_t)N : 0;
+    for (BatchSet& b : c->gsets)
+        if (rv_status as = bset_alloc(c, b, F, tiles ? slice : 0, gneed)) return as;
+    const size_t nstage = 3 * (size_t)F * chunk, nall = 3 * (size_t)Nrec * F * chunk;
+    if (c->grec_stage_n < nstage || c->grec_all_n < nall || c->gring_n < cap) {
+        HIP_TRY(c, hipDeviceSynchronize());
+        hipFree(c->grec_stage); hipFree(c->grec_all); hipFree(c->gring);
+        c->grec_stage = nullptr; c->grec_all = nullptr; c->gring = nullptr;
+        c->grec_stage_n = c->grec_all_n = c->gring_n = 0;
+        HIP_TRY(c, hipMalloc(&c->grec_stage, nstage * sizeof(uint2)));
+        HIP_TRY(c, hipMalloc(&c->grec_all, nall * sizeof(uint2)));
+        HIP_TRY(c, hipMalloc(&c->gring, cap * 4));
+        c->grec_stage_n = nstage; c->grec_all_n = nall; c->gring_n = cap;
+        // a record slot nobody wrote (other ranks' chunks under the timing probe) reads as a solid cell
+        HIP_TRY(c, hipMemset(c->grec_all, 0, nall * sizeof(uint2)));
+    }
+    for (hipEvent_t& e : c->gev)
+        if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipEvent_t& ev_rendered = c->gev[0];
+    hipEvent_t& ev_applied = c->gev[1];
+    hipEvent_t& ev_allg = c->gev[2];
+    hipEvent_t* ev_pb = &c->gev[3];        // [2] phase B of group h done (slot h & 1)
+    hipEvent_t* ev_gath = &c->gev[5];      // [2] tile gather of group g done (slot g & 1)
+    hipEvent_t& ev_tmp = c->gev[7];
+    if (!c->grp_stream) HIP_TRY(c, hipStreamCreateWithPriority(&c->grp_stream, hipStreamNonBlocking, c->prio_hi));
+    hipStream_t SB = c->grp_stream;
+    slot_save(c);
+    slot_load(c, 0);
+    c->stream = S;
+    if (rv_status ws = wait_all_frames(c)) return ws;   // frames of earlier calls, the last world write
+    c->carry_gi = c->carry_pp = false;                 // the per-frame pipeline's kept work is stale now
+    HIP_TRY(c, hipEventRecord(ev_tmp, S));             // SB and the comm stream start after that too
+    HIP_TRY(c, hipStreamWaitEvent(SB, ev_tmp, 0));
+    if (xchg) HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ev_tmp, 0));
+    if (tiles) {
+        if (rv_status us = upload_ids(c, c->untile_ids, c->shard_all.data(), (int)c->shard_all.size(), nullptr)) return us;
+        if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
+    }
+    const FrameCam* cams = nullptr;
+    if (rv_status us = upload_cams(c, q, S, &cams)) return us;
+    // the GI window of every frame of the call (rv_update_gi_data's sequence) and its ring position
+    std::vector<uint32_t> wfr((size_t)frames), wfirst((size_t)frames), wcount((size_t)frames), wpos((size_t)frames + 1);
+    {
+        uint64_t off = c->gi_offset, pos = 0;
+        for (int k = 0; k < frames; k++) {
+            wfr[(size_t)k] = c->gi_frame + (uint32_t)k;
+            wfirst[(size_t)k] = (uint32_t)off;
+            wcount[(size_t)k] = (uint32_t)(off + rays > ngi ? ngi - off : rays);
+            wpos[(size_t)k] = (uint32_t)(pos & cmask);
+            pos += wcount[(size_t)k];
+            off = off + rays >= ngi ? 0 : off + rays;   // src/CoarseArray.cu:392-394
+        }
+        wpos[(size_t)frames] = (uint32_t)(pos & cmask);
+    }
+    auto gsum = [&](int g, int j) {   // cells of group g's updates before its j-th
+        uint64_t t = 0;
+        for (int k = g * F; k < g * F + j; k++) t += wcount[(size_t)k];
+        return (uint32_t)t;
+    };
+    const World w = current_world(c);
+    const int tiles_x = (W + T - 1) / std::max(T, 1);
+    const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
+
+    // phase A of group h, window j: this rank's cells and its record slot
+    auto window_share = [&](int k, uint32_t& mfirst, uint32_t& mine) {
+        mfirst = wfirst[(size_t)k]; mine = wcount[(size_t)k];
+        if (shard_gi) {
+            mfirst = wfirst[(size_t)k] + (uint32_t)std::min<uint64_t>(wcount[(size_t)k], (uint64_t)R * chunk);
+            mine = (uint32_t)std::min<uint64_t>(chunk, (uint64_t)wfirst[(size_t)k] + wcount[(size_t)k] - mfirst);
+        }
+    };
+    auto rec_base = [&](int h) -> uint2* {   // where launch phase A writes group h's records
+        return xchg ? c->grec_stage + (size_t)(h % 3) * F * chunk : c->grec_all + (size_t)(h % 3) * Nrec * F * chunk;
+    };
+    auto add_phase_a = [&](GroupParams& gp, int h) {
+        uint2* base = rec_base(h);
+        for (int j = 0; j < nfr(h); j++) {
+            const int k = h * F + j, x = (int)gp.nw++;
+            uint32_t mf, mine;
+            window_share(k, mf, mine);
+            gp.g_frame[x] = wfr[(size_t)k]; gp.g_first[x] = mf; gp.g_count[x] = mine;
+            gp.g_rec[x] = (uint32_t)((base - gp.rec) + (size_t)j * chunk);
+        }
+    };
+    auto launch_group = [&](int g, bool timed) -> rv_status {
+        // render part: group g (none in the prologue, g = -1); pre-pass of group g+1; phase A: group g+2
+        // (the prologue: groups 0 and 1)
+        FrameParams f = make_params_d(c, q.at(std::max(g, 0) * F), flags);
+        f.cams = cams + (size_t)std::max(g, 0) * F;
+        const BatchSet& bs = c->gsets[std::max(g, 0) & 1];
+        f.color = bs.color; f.mv = bs.mv; f.depth = bs.depth;
+        f.color_pitch = c->own_color_pitch; f.mv_pitch = c->own_mv_pitch; f.depth_pitch = c->own_depth_pitch;
+        f.bs_color = cstride; f.bs_mv = mstride; f.bs_depth = dstride;
+        f.hdist = bs.hdist; f.hshadow = bs.hshadow; f.bs_half = hbytes;
+        f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
+        if (tiles) {
+            f.tiles = c->tiles.d; f.ntiles = (int)c->shard_ids.size(); f.tile_px = T; f.tiles_x = tiles_x;
+            f.tilebuf = bs.tbuf; f.tile_bpp = bpp; f.bs_tile = slice;
+            f.chunk_order[CG_RENDER] = c->tile_order; f.chunk_cost[CG_RENDER] = c->tile_cost;
+        }
+        GroupParams gp{};
+        gp.nr = g >= 0 ? (uint32_t)nfr(g) : 0u;
+        f.nbatch = std::max(gp.nr, 1u);
+        gp.rlen1 = pipe_len(f, PIPE_RENDER, 0);
+        gp.ov = c->gring; gp.gmask = gmask; gp.cmask = cmask;
+        if (g >= 0) {
+            gp.ov_s = wfirst[(size_t)g * F]; gp.ov_p = wpos[(size_t)g * F];
+            for (uint32_t j = 0; j < gp.nr; j++) gp.ov_len[j] = gsum(g, (int)j + 1);   // frame j sees its own update
+        }
+        const int hp = g + 1;   // the pre-pass's group
+        gp.np = (uint32_t)nfr(hp);
+        gp.plen1 = pipe_len(f, PIPE_PP, 0);
+        if (gp.np) {
+            gp.pcams = cams + (size_t)hp * F;
+            gp.pp_hdist = c->gsets[hp & 1].hdist; gp.pp_hshadow = c->gsets[hp & 1].hshadow; gp.pp_bs = hbytes;
+        }
+        gp.rec = xchg ? c->grec_stage : c->grec_all;
+        gp.glen1 = (uint32_t)(((chunk + 63) / 64 + 7) & ~7ull);
+        if (g < 0) { add_phase_a(gp, 0); add_phase_a(gp, 1); } else { add_phase_a(gp, g + 2); }
+        gp.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
+        gp.gi_counters = c->counters + (size_t)ST_GI * NCNT;
+        const uint32_t lens[3] = {gp.nw * gp.glen1, gp.np * gp.plen1, gp.nr * gp.rlen1};
+        for (int i = 0; i < 3; i++) {
+            gp.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;
+            gp.len[i] = lens[gp.part[i]];
+        }
+        const bool tm = timed && c->timing_n < c->timing_cap;
+        const size_t e0 = (size_t)EV_PER_FRAME * c->timing_n;
+        if (tm) { c->ev_stage[e0] = ST_PRIMARY; HIP_TRY(c, hipEventRecord(c->ev[e0], S)); }
+        launch_ref_group(S, w, f, gp);
+        LAUNCH_CHECK(c);
+        if (tm) {
+            c->ev_stage[e0 + 1] = -1;
+            HIP_TRY(c, hipEventRecord(c->ev[e0 + 1], S));
+            c->ev_used[c->timing_n] = 2;
+            c->timing_n++;
+        }
+        return RV_OK;
+    };
+    // phase B of group h on stream st: window j reads grid (frame before it) through the overlay of
+    // origin group o = max(h - 1, 0)
+    auto phase_b = [&](int h, hipStream_t st) -> rv_status {
+        const int o = std::max(h - 1, 0);
+        WorldOv wo;
+        static_cast<World&>(wo) = w;
+        wo.ov = c->gring; wo.gmask = gmask; wo.cmask = cmask;
+        wo.ov_s = wfirst[(size_t)o * F]; wo.ov_p = wpos[(size_t)o * F];
+        const uint2* recs = c->grec_all + (size_t)(h % 3) * Nrec * F * chunk;
+        for (int j = 0; j < nfr(h); j++) {
+            const int k = h * F + j;
+            wo.ov_len = (h > 0 ? gsum(o, nfr(o)) : 0u) + gsum(h, j);
+            const uint32_t dpos = (wo.ov_p + ((wfirst[(size_t)k] - wo.ov_s) & gmask)) & cmask;
+            launch_gi_phase_b(st, wo, recs, (uint32_t)chunk, (uint32_t)F, (uint32_t)j, wfirst[(size_t)k],
+                              wcount[(size_t)k], c->gring, dpos);
+            LAUNCH_CHECK(c);
+        }
+        return RV_OK;
+    };
+    auto allgather = [&](int h) -> rv_status {   // group h's records from every rank (comm stream)
+        if (rv_status as = comm_all_gather(c, comm, c->grec_stage + (size_t)(h % 3) * F * chunk,
+                                           c->grec_all + (size_t)(h % 3) * Nrec * F * chunk,
+                                           (size_t)F * chunk * sizeof(uint2), c->comm_stream))
+            return as;
+        HIP_TRY(c, hipEventRecord(ev_allg, c->comm_stream));
+        return RV_OK;
+    };
+    auto untile = [&](int g) -> rv_status {   // rank 0: assemble group g once its gather is done
+        HIP_TRY(c, hipStreamWaitEvent(S, ev_gath[g & 1], 0));
+        launch_untile(S, c->gsets[g & 1].gbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tiles_x, W, H,
+                      c->gsets[g & 1].color, c->own_color_pitch, c->shard_max, nfr(g), cstride, bpp);
+        LAUNCH_CHECK(c);
+        return RV_OK;
+    };
+
+    // ---- prologue
+    if (rv_status ls = launch_group(-1, false)) return ls;
+    HIP_TRY(c, hipEventRecord(ev_rendered, S));
+    if (xchg) {
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ev_rendered, 0));
+        if (rv_status as = allgather(0)) return as;
+        HIP_TRY(c, hipStreamWaitEvent(S, ev_allg, 0));
+    }
+    if (rv_status ps = phase_b(0, S)) return ps;
+    if (G > 1) {
+        HIP_TRY(c, hipEventRecord(ev_tmp, S));   // phase B of group 0 written (group 1 reads it)
+        HIP_TRY(c, hipStreamWaitEvent(SB, ev_tmp, 0));
+        if (xchg) {
+            if (rv_status as = allgather(1)) return as;
+            HIP_TRY(c, hipStreamWaitEvent(SB, ev_allg, 0));
+        }
+        if (rv_status ps = phase_b(1, SB)) return ps;
+        HIP_TRY(c, hipEventRecord(ev_pb[1], SB));
+    }
+    // ---- groups
+    for (int g = 0; g < G; g++) {
+        if (g >= 1) HIP_TRY(c, hipStreamWaitEvent(S, ev_pb[g & 1], 0));
+        if (xchg && g >= 2) HIP_TRY(c, hipStreamWaitEvent(S, ev_gath[g & 1], 0));   // tile buffers of group g-2 sent
+        if (rv_status ls = launch_group(g, nfr(g) == F)) return ls;
+        HIP_TRY(c, hipEventRecord(ev_rendered, S));
+        launch_gi_apply(S, c->gring, c->gi, wfirst[(size_t)g * F], wpos[(size_t)g * F], gsum(g, nfr(g)), gmask, cmask);
+        LAUNCH_CHECK(c);
+        HIP_TRY(c, hipEventRecord(ev_applied, S));
+        FrameParams fo = make_params_d(c, q.at(g * F), flags);   // SCHED_COST re-order after every group
+        if (fo.sched == SCHED_COST) {
+            if (tiles) {
+                const uint32_t nt = (uint32_t)c->shard_ids.size();
+                launch_chunk_order(S, c->tile_cost, c->tile_order, nt, (nt + 7u) & ~7u);
+            } else {
+                launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(fo.hw, fo.hh),
+                                   n_chunks_pad(fo.hw, fo.hh));
+                launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(W, H),
+                                   n_chunks_pad(W, H));
+            }
+            LAUNCH_CHECK(c);
+        }
+        if (xchg) {
+            HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ev_rendered, 0));
+            if (g + 2 < G)
+                if (rv_status as = allgather(g + 2)) return as;
+            // the group's packed tiles to rank 0
+            const BatchSet& bs = c->gsets[g & 1];
+            const size_t sb = slice * (size_t)nfr(g);
+            if (root) HIP_TRY(c, hipMemcpyAsync(bs.gbuf, bs.tbuf, sb, hipMemcpyDeviceToDevice, c->comm_stream));
+            if (rv_status gs = comm_group_start(c, comm)) return gs;
+            if (root) {
+                for (int r = 1; r < N; r++)
+                    if (rv_status rs = comm_recv(c, comm, reinterpret_cast<char*>(bs.gbuf) + (size_t)r * sb, sb, r,
+                                                 c->comm_stream))
+                        return rs;
+            } else {
+                if (rv_status ss = comm_send(c, comm, bs.tbuf, sb, 0, c->comm_stream)) return ss;
+            }
+            if (rv_status ge = comm_group_end(c, comm, c->comm_stream)) return ge;
+            HIP_TRY(c, hipEventRecord(ev_gath[g & 1], c->comm_stream));
+        }
+        if (g + 2 < G) {   // phase B of group g+2 overlaps launch g+1
+            HIP_TRY(c, hipStreamWaitEvent(SB, ev_applied, 0));
+            HIP_TRY(c, hipStreamWaitEvent(SB, xchg ? ev_allg : ev_rendered, 0));
+            if (rv_status ps = phase_b(g + 2, SB)) return ps;
+            HIP_TRY(c, hipEventRecord(ev_pb[g & 1], SB));
+        }
+        if (xchg && root && g >= 1)
+            if (rv_status us = untile(g - 1)) return us;
+        if (tiles && !xchg && N == 1) {   // one rank without a communicator: assemble locally
+            launch_untile(S, c->gsets[g & 1].tbuf, c->untile_ids.d, (int)c->shard_all.size(), T, tiles_x, W, H,
+                          c->gsets[g & 1].color, c->own_color_pitch, c->shard_max, nfr(g), cstride, bpp);
+            LAUNCH_CHECK(c);
+        }
+        c->frame_seq += (uint64_t)nfr(g);
+    }
+    if (xchg) {
+        if (root)
+            if (rv_status us = untile(G - 1)) return us;
+        HIP_TRY(c, hipEventRecord(ev_tmp, c->comm_stream));   // S sees the last gather done
+        HIP_TRY(c, hipStreamWaitEvent(S, ev_tmp, 0));
+    }
+    // the GI counters advance by the frames rendered; the last frame becomes the slot's output
+    c->gi_frame += (uint32_t)frames;
+    c->gi_offset = frames > 0 ? (wfirst[(size_t)frames - 1] + rays >= ngi ? 0 : wfirst[(size_t)frames - 1] + rays)
+                              : c->gi_offset;
+    if (rv_status ps = bset_publish(c, c->gsets[(G - 1) & 1], (size_t)nfr(G - 1) - 1, true, S)) return ps;
+    if (rv_status ms = mark_world(c)) return ms;
+    FrameSlot& s0 = c->slots[0];
+    HIP_TRY(c, hipEventRecord(s0.done, S));
+    s0.pending = true;
+    s0.last_stream = S;
+    return RV_OK;
+}
+
+extern "C" rv_status rv_get_frame_group(rv_ctx* c, int32_t* effective) {
+    if (!c || !effective) return RV_ERR_INVALID;
+    *effective = c->pipe && c->megakernel ? group_frames(c) : 0;
+    return RV_OK;
+}
+
 // Batched frame loop: groups of B = (frame slots) frames, each group one
 // launch per stage with the frame index in the grid (FrameParams::nbatch),
 // one RCCL gather of the group's packed tiles and one untile.  Group j runs
@@ -2265,6 +2601,8 @@ static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
     mix((uint64_t)comm->nranks); mix((uint64_t)c->shard_n); mix((uint64_t)c->shard_px); mix((uint64_t)c->gather_bpp);
     mix(w0); mix((uint64_t)c->shard_max); mix((uint64_t)c->cfg.width); mix((uint64_t)c->cfg.height);
     mix((uint64_t)c->cfg.gi_rays_per_frame); mix((uint64_t)(flags & ~RV_F_STATS));
+    // the loop kind shapes the exchanges too (grouped frames: the group size)
+    mix((uint64_t)((flags & RV_F_STATS) ? 0 : group_frames(c))); mix((uint64_t)c->pipe);
     for (int32_t t : c->shard_all) mix((uint64_t)(uint32_t)t);
     if (!c->comm_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     uint64_t* d = nullptr;
@@ -2289,7 +2627,6 @@ static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
 
 static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_per_frame, rv_comm* comm) {
     const int frames = q.n;
-    if (c->cfg.ref_compat) flags |= RV_F_REF_FETCH;   // as rv_draw_cuda: the minDist fetch of a ref_compat context
     if (comm) {
         // a communicator belongs to the context it was created on (rv_comm_destroy
         // detaches only that one, rv_sync / rv_destroy wait on it)
@@ -2351,6 +2688,16 @@ static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_p
         c->ext_tilebuf = saved_ext; c->ext_tilebuf_bytes = saved_ext_bytes;
         c->stream = caller;
         return st;
+    }
+    const int gF = group_frames(c);
+    if (gi_per_frame && (flags & RV_F_PREPASS) && c->pipe && c->megakernel && frames > 0 && gF >= 2 &&
+        !(flags & RV_F_STATS)) {
+        hipStream_t S = own0 ? c->fstreams[0] : caller;
+        st = render_gi_group(c, q, flags, S, comm, gF);
+        c->stream = caller;
+        if (st != RV_OK) return st;
+        if (S != caller) HIP_TRY(c, hipStreamWaitEvent(caller, c->slots[0].done, 0));
+        return RV_OK;
     }
     if (gi_per_frame && (flags & RV_F_PREPASS) && c->pipe && c->megakernel && frames > 0) {
         hipStream_t S = own0 ? c->fstreams[0] : caller;

@@ -374,6 +374,21 @@ RV_HD uint32_t voxel_word_nc(const LinearWorld& w, uint32_t x, uint32_t y, uint3
 // 512 B of CSDF) staged in LDS (RV_PRIMARY_TILE): gathers that fall inside the
 // tile read LDS (~50-cycle latency) instead of the vector L1/L2 path; the rest
 // read the world.  The tile is wave-uniform (tbx.. from the wave's first lane).
+// GI grid with an overlay of updates not yet copied into it (grouped reference
+// frames, rv_set_frame_group): the cells of the contiguous range [ov_s, ov_s +
+// ov_len) (mod the grid size) are read from the ring `ov` at position ov_p +
+// (cell - ov_s); every other cell from the grid.  Only gi_texel differs from
+// World, so a frame rendered with it sees the grid of its own frame while the
+// grid itself still holds an older frame's.
+struct WorldOv : World {
+    const uint32_t* __restrict__ ov;
+    uint32_t ov_s, ov_p, ov_len, gmask, cmask;
+};
+RV_HD uint32_t gi_texel(const WorldOv& w, uint32_t idx) {
+    const uint32_t off = (idx - w.ov_s) & w.gmask;
+    return off < w.ov_len ? w.ov[(w.ov_p + off) & w.cmask] : w.gi[idx];
+}
+
 struct WorldTile : World {
     const uint32_t* tile;   // LDS: [brick (k*2+j)*2+i][16 dwords] bits, then the same for the CSDF
     uint32_t tbx, tby, tbz;
@@ -1080,7 +1095,15 @@ RV_HD f3 sample_sky(f3 dir, f3 sun) {
 // +121.3 offsets added in double (:43), swapped atlas coords (R10),
 // point filter + wrap on a 256x256 RGBA8 atlas, texel = byte/255.
 template <class WV>
+RV_HD uint32_t sample_texel(const WV& w, float u, float v, f3 pos);
+RV_HD f3 texel_rgb(uint32_t t) { return V(u8f(t & 255u), u8f((t >> 8) & 255u), u8f((t >> 16) & 255u)); }
+template <class WV>
 RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
+    return texel_rgb(sample_texel(w, u, v, pos));
+}
+// the atlas texel sampleTexture reads (its colour is texel_rgb of it)
+template <class WV>
+RV_HD uint32_t sample_texel(const WV& w, float u, float v, f3 pos) {
     const float freq = 0.05f;
     float e = 0.5f;
     if (!(RV_ABLATE & 1)) {
@@ -1108,10 +1131,8 @@ RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
     int row = imin((int)floorf(cv * (float)w.ah), w.ah - 1);
     RV_GD_KIND(gd::TEX);
     RV_GD(0, w.atlas + row * w.aw + col);
-    const uint32_t t = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.atlas) +
-                                                          4u * (uint32_t)(row * w.aw + col));
-    return V(u8f(t & 255u), u8f((t >> 8) & 255u),
-             u8f((t >> 16) & 255u));
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.atlas) +
+                                              4u * (uint32_t)(row * w.aw + col));
 }
 
 }  // namespace rv

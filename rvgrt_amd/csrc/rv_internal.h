@@ -106,6 +106,37 @@ struct PipeParams {
     uint32_t* wave_max;     // diagnostics (env RV_PIPE_WAVE_STATS): per workgroup, part << 30 | 10-ns ticks
 };
 
+// Grouped reference frames (rv_set_frame_group): one launch
+// renders a group of frames, runs the pre-pass of the next group and phase A
+// of the GI updates of the group after that.  The GI update is split: phase A
+// traces a cell's shadow and bounce rays (the static world only) into an 8-B
+// record (GIRec); phase B (k_gi_phase_b, a small kernel per update) combines
+// the record with the grid the update reads.  Updates not yet copied into the
+// grid live in a ring of cells and are read through WorldOv.
+enum { GRP_MAX = 32 };   // windows (GI updates) of one launch's phase A part; frames <= GRP_MAX / 2
+// record: a = kind << 28 | bounce hit cell (28 bits) | lit << 31; b = atlas texel (GR_HIT) or the
+// sky blend t as float bits (GR_MISS)
+enum : uint32_t { GR_SOLID = 0, GR_HIT = 1, GR_HIT_OOB = 2, GR_MISS = 3, GR_MISS_SUN = 4 };
+struct GroupParams {
+    uint32_t part[3], len[3];     // as PipeParams: part[i] dispatched i-th over len[i] workgroups
+    // render part: nr frames of rlen1 workgroups; frame j: FrameParams::cams[j], outputs at the
+    // bs_* strides, GI overlay length ov_len[j] (origin ov_s / ov_p shared by the group)
+    uint32_t nr, rlen1;
+    const uint32_t* ov; uint32_t ov_s, ov_p, gmask, cmask;
+    uint32_t ov_len[GRP_MAX / 2];
+    // pre-pass part: np frames of plen1 workgroups; frame j: camera pcams[j], images + j * pp_bs
+    uint32_t np, plen1;
+    const FrameCam* pcams;
+    float* pp_hdist; float* pp_hshadow; uint64_t pp_bs;
+    // GI record part (phase A): nw windows of glen1 workgroups; window j: GI frame number
+    // g_frame[j], this rank's cells [g_first[j], + g_count[j]) into rec + g_rec[j]
+    uint32_t nw, glen1;
+    uint32_t g_frame[GRP_MAX], g_first[GRP_MAX], g_count[GRP_MAX], g_rec[GRP_MAX];
+    uint2* rec;
+    unsigned long long* pp_counters;
+    unsigned long long* gi_counters;
+};
+
 struct RvHitDev {   // == rv_hit
     float pos[3], normal[3], u, v;
     int hit, undef, sphere, dda, check, pad;
@@ -129,6 +160,15 @@ void launch_render(hipStream_t s, const World& w, const FrameParams& f);
 // workgroups of each part of a pipelined launch; then the launch itself
 uint32_t pipe_len(const FrameParams& f, int part, uint64_t gi_count);
 void launch_ref_pipe(hipStream_t s, const World& w, const FrameParams& f, const PipeParams& p);
+// grouped reference frames: the launch (GroupParams) and the GI update's phase B over one window
+// (cells [first, first + count) of GI frame `frame`, records rec[((q / chunk) * nwin + j) * chunk
+// + q % chunk] for cell first + q; output to ring position (dpos + q) & w.cmask) and the
+// copy of len ring cells from position p into the grid at cell s (wrapping mod the grid)
+void launch_ref_group(hipStream_t s, const World& w, const FrameParams& f, const GroupParams& g);
+void launch_gi_phase_b(hipStream_t s, const WorldOv& w, const uint2* rec, uint32_t chunk, uint32_t nwin,
+                       uint32_t j, uint32_t first, uint32_t count, uint32_t* ring, uint32_t dpos);
+void launch_gi_apply(hipStream_t s, const uint32_t* ring, uint32_t* gi, uint32_t sc, uint32_t p, uint32_t len,
+                     uint32_t gmask, uint32_t cmask);
 // SCHED_COST: sort n costs (order has npad >= n entries) into a descending
 // order, clearing the costs
 void launch_chunk_order(hipStream_t s, uint32_t* cost, int* order, uint32_t n, uint32_t npad);

@@ -200,6 +200,16 @@ class StateRender:
         """rv_set_pipeline: pipelined reference frames in render_frames."""
         self._check(self._L.rv_set_pipeline(self._h, int(bool(on))), "rv_set_pipeline")
 
+    def set_frame_group(self, n):
+        """rv_set_frame_group: reference frames rendered n per launch (0 = off)."""
+        self._check(self._L.rv_set_frame_group(self._h, int(n)), "rv_set_frame_group")
+
+    def frame_group_effective(self):
+        """The group size render_frames will use (0: per-frame pipeline)."""
+        v = C.c_int32(0)
+        self._check(self._L.rv_get_frame_group(self._h, C.byref(v)), "rv_get_frame_group")
+        return int(v.value)
+
     def set_gi_stats(self, on):
         """rv_set_gi_stats: count the GI update's traversal steps (stage 'gi')."""
         self._check(self._L.rv_set_gi_stats(self._h, int(bool(on))), "rv_set_gi_stats")

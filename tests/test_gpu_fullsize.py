@@ -209,10 +209,10 @@ def test_reference_native_config_draw_cuda(rv, atlas, oracle):
     r.close()
 
 
-@pytest.mark.parametrize("cfgname", ["c3", "c4"])
-def test_fullsize_pipelined_frames(rv, atlas, cfgname):
+@pytest.mark.parametrize("cfgname,grp", [("c3", 0), ("c4", 0), ("c3", 8), ("c4", 8)])
+def test_fullsize_pipelined_frames(rv, atlas, cfgname, grp):
     """The C3/C4 frame loop as bench.py runs it (pipelined launches: render
-    k | GI update k+1 | pre-pass k+1) against UpdateGIData + drawCUDA one
+    k | GI update k+1 | pre-pass k+1; or grouped: 8 frames per launch) against UpdateGIData + drawCUDA one
     frame at a time on the same full-size world: colour, depth and the GI
     grid bit-identical after 6 frames (the one-at-a-time frames are checked
     against the oracle by the tests above)."""
@@ -227,10 +227,12 @@ def test_fullsize_pipelined_frames(rv, atlas, cfgname):
         for s in range(max(cfg.gi_sweeps, 0)):
             r.gi_update(s)
         r.set_pipeline(pipe)
+        nf = 12 if grp else 6    # grouped: 8 frames per launch, the call ends mid-group
         if pipe:
-            r.render_frames(6, cam, vp, gi_per_frame=True)
+            r.set_frame_group(grp)
+            r.render_frames(nf, cam, vp, gi_per_frame=True)
         else:
-            for _ in range(6):
+            for _ in range(nf):
                 r.update_gi_data()
                 r.frame(cam, vp)
         r.sync()

@@ -54,12 +54,14 @@ def _run_ranks(fns):
             raise e
 
 
-@pytest.mark.parametrize("flags,T,N,w0,bpp", [
-    (8, 16, 2, 1.0, 3), (8, 16, 3, 0.9, 4), (8, 32, 8, 0.87, 3),       # batched groups (C1/C2 loop)
-    (7, 32, 2, 1.0, 3), (7, 32, 3, 0.94, 4), (7, 16, 8, 0.87, 3),      # pipelined reference frames (C3-C5 loop)
-    (7, 64, 2, 0.98, 3), (7, 64, 4, 0.94, 4),                         # the bench's reference-frame tile size
+@pytest.mark.parametrize("flags,T,N,w0,bpp,grp", [
+    (8, 16, 2, 1.0, 3, 0), (8, 16, 3, 0.9, 4, 0), (8, 32, 8, 0.87, 3, 0),       # batched groups (C1/C2 loop)
+    (7, 32, 2, 1.0, 3, 0), (7, 32, 3, 0.94, 4, 0), (7, 16, 8, 0.87, 3, 0),      # pipelined reference frames
+    (7, 64, 2, 0.98, 3, 0), (7, 64, 4, 0.94, 4, 0),                         # the bench's reference-frame tile size
+    (7, 64, 2, 0.98, 3, 3), (7, 32, 3, 0.94, 4, 2), (7, 64, 4, 0.94, 3, 3),    # grouped reference frames: sharded
+    (7, 16, 8, 0.87, 3, 3),                                                 # phase A, record all-gather per group
 ])
-def test_loopback_ranks_equal_one_context(rv, atlas, flags, T, N, w0, bpp):
+def test_loopback_ranks_equal_one_context(rv, atlas, flags, T, N, w0, bpp, grp):
     from rvgrt_amd.configs import TEST_POSES_128, camera_path
     gi = bool(flags & rv.RV_F_GI)
     seq = camera_path(TEST_POSES_128["P0"], W, H, 11, pan=0.02, ref_compat=True)
@@ -73,6 +75,7 @@ def test_loopback_ranks_equal_one_context(rv, atlas, flags, T, N, w0, bpp):
             r.set_frames_in_flight(4)
         r.set_tile_shard(T, q, N, root_weight=w0)
         r.set_gather_bpp(bpp)
+        r.set_frame_group(grp)
         comms.append(rv.Comm.loopback(r, group, q))
     done = 0
     for a, b, nxt in ((0, 4, 4), (4, 11, None)):   # two calls: the second starts from the kept work

@@ -49,7 +49,10 @@ def main():
     pos, yaw, pitch = pose_f32(cfg)
     cam, vp = rv.camera_from_pose(pos, yaw, pitch, W, H)
     frames = max(4 * K, 32)   # the pipelined GI loop's prologue amortised over the call
+    if int(os.environ.get("SHARD_GROUP", "0")) >= 2:
+        frames = 128          # grouped frames: a longer call for the group loop's prologue
     r.set_frames_in_flight(K)
+    r.set_frame_group(int(os.environ.get("SHARD_GROUP", "0")))   # grouped reference frames
     r.set_tile_shard(64, 0, 0)
     gi = cfg.gi_per_frame
     full = per_frame_us(r, cam, vp, frames, gi)
