@@ -635,13 +635,18 @@ rv_status rv_csdf_build(rv_ctx* c) {
     if (rv_status ws = wait_all_frames(c)) return ws;
     c->geom_ver++;
     uint64_t n = n_csdf(c);
+    // Scratch of the three passes: plain allocations, freed after the build completed.  (Stream-
+    // ordered hipMallocAsync scratch on the legacy stream was measured to overlap allocations of
+    // later contexts' grouped-frame buffers in the same process: sporadically corrupted CSDF.)
     uint8_t *t0 = nullptr, *t1 = nullptr;
-    HIP_TRY(c, hipMallocAsync((void**)&t0, n, c->stream));
-    HIP_TRY(c, hipMallocAsync((void**)&t1, n, c->stream));
+    HIP_TRY(c, hipMalloc((void**)&t0, n));
+    HIP_TRY(c, hipMalloc((void**)&t1, n));
     launch_csdf(c->stream, c->brick, current_world(c), t0, t1);
     LAUNCH_CHECK(c);
-    HIP_TRY(c, hipFreeAsync(t0, c->stream));
-    HIP_TRY(c, hipFreeAsync(t1, c->stream));
+    const hipError_t se = hipStreamSynchronize(c->stream);
+    hipFree(t0);
+    hipFree(t1);
+    HIP_TRY(c, se);
     return mark_world(c);
 }
 
@@ -2054,8 +2059,9 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
         HIP_TRY(c, hipMalloc(&c->grec_all, nall * sizeof(uint2)));
         HIP_TRY(c, hipMalloc(&c->gring, cap * 4));
         c->grec_stage_n = nstage; c->grec_all_n = nall; c->gring_n = cap;
-        // a record slot nobody wrote (other ranks' chunks under the timing probe) reads as a solid cell
-        HIP_TRY(c, hipMemset(c->grec_all, 0, nall * sizeof(uint2)));
+        // a record slot nobody wrote (other ranks' chunks under the timing probe) reads as a solid cell;
+        // on S: a plain hipMemset runs on the legacy stream, which does not order with S
+        HIP_TRY(c, hipMemsetAsync(c->grec_all, 0, nall * sizeof(uint2), S));
     }
     for (hipEvent_t& e : c->gev)
         if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
