@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <tuple>
@@ -863,7 +864,8 @@ static FrameCam frame_cam(const rv_frame_desc& d) {
 // Uploads the cameras of all frames of a sequence (batched launches index it
 // from their first frame) on stream st; returns the device table.  The
 // pinned staging buffer is reused only after its last upload has executed.
-static rv_status upload_cams(rv_ctx* c, const Seq& q, hipStream_t st, const FrameCam** out) {
+static rv_status upload_cams(rv_ctx* c, const Seq& q, hipStream_t st, const FrameCam** out,
+                             const std::function<void(int, FrameCam&)>& fill = nullptr) {
     const size_t n = (size_t)q.n;
     if (c->cam_pending) HIP_TRY(c, hipEventSynchronize(c->cam_ev));
     if (n > c->cam_cap) {
@@ -877,13 +879,17 @@ static rv_status upload_cams(rv_ctx* c, const Seq& q, hipStream_t st, const Fram
         c->cam_cap = cap;
     }
     if (!c->cam_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->cam_ev, hipEventDisableTiming));
-    for (size_t k = 0; k < n; k++) c->cam_host[k] = frame_cam(q.at((int)k));
+    for (size_t k = 0; k < n; k++) {
+        c->cam_host[k] = frame_cam(q.at((int)k));
+        if (fill) fill((int)k, c->cam_host[k]);
+    }
     HIP_TRY(c, hipMemcpyAsync(c->cam_dev, c->cam_host, n * sizeof(FrameCam), hipMemcpyHostToDevice, st));
     HIP_TRY(c, hipEventRecord(c->cam_ev, st));
     c->cam_pending = true;
     *out = c->cam_dev;
     return RV_OK;
 }
+
 
 // Enqueue the frame's stages, recording a start event per stage when timing
 // is on.  Each stage counts into its own counter block (rv_stats_stage).
@@ -2085,8 +2091,6 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
         if (rv_status us = upload_ids(c, c->untile_ids, c->shard_all.data(), (int)c->shard_all.size(), nullptr)) return us;
         if (rv_status ts = tile_list(c, c->shard_ids.data(), (int32_t)c->shard_ids.size(), T)) return ts;
     }
-    const FrameCam* cams = nullptr;
-    if (rv_status us = upload_cams(c, q, S, &cams)) return us;
     // the GI window of every frame of the call (rv_update_gi_data's sequence) and its ring position
     std::vector<uint32_t> wfr((size_t)frames), wfirst((size_t)frames), wcount((size_t)frames), wpos((size_t)frames + 1);
     {
@@ -2106,11 +2110,7 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
         for (int k = g * F; k < g * F + j; k++) t += wcount[(size_t)k];
         return (uint32_t)t;
     };
-    const World w = current_world(c);
-    const int tiles_x = (W + T - 1) / std::max(T, 1);
-    const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
-
-    // phase A of group h, window j: this rank's cells and its record slot
+    // phase A of frame k's update: this rank's cells of its window
     auto window_share = [&](int k, uint32_t& mfirst, uint32_t& mine) {
         mfirst = wfirst[(size_t)k]; mine = wcount[(size_t)k];
         if (shard_gi) {
@@ -2118,18 +2118,25 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
             mine = (uint32_t)std::min<uint64_t>(chunk, (uint64_t)wfirst[(size_t)k] + wcount[(size_t)k] - mfirst);
         }
     };
-    auto rec_base = [&](int h) -> uint2* {   // where launch phase A writes group h's records
-        return xchg ? c->grec_stage + (size_t)(h % 3) * F * chunk : c->grec_all + (size_t)(h % 3) * Nrec * F * chunk;
-    };
-    auto add_phase_a = [&](GroupParams& gp, int h) {
-        uint2* base = rec_base(h);
-        for (int j = 0; j < nfr(h); j++) {
-            const int k = h * F + j, x = (int)gp.nw++;
-            uint32_t mf, mine;
-            window_share(k, mf, mine);
-            gp.g_frame[x] = wfr[(size_t)k]; gp.g_first[x] = mf; gp.g_count[x] = mine;
-            gp.g_rec[x] = (uint32_t)((base - gp.rec) + (size_t)j * chunk);
-        }
+    // the per-frame table the launches read: camera, this rank's phase A cells, overlay length
+    const FrameCam* cams = nullptr;
+    if (rv_status us = upload_cams(c, q, S, &cams, [&](int k, FrameCam& fc) {
+            window_share(k, fc.gi_first, fc.gi_count);
+            fc.gi_ovlen = gsum(k / F, k % F + 1);   // frame k sees its own update
+        }))
+        return us;
+    const World w = current_world(c);
+    const int tiles_x = (W + T - 1) / std::max(T, 1);
+    const size_t cstride = c->own_color_pitch * H, mstride = c->own_mv_pitch * H, dstride = c->own_depth_pitch * H;
+
+    // phase A of groups [h0, h1): their frames are consecutive, window j = frame h0 * F + j
+    auto set_phase_a = [&](GroupParams& gp, int h0, int h1) {
+        gp.nw = 0;
+        for (int h = h0; h < h1; h++) gp.nw += (uint32_t)nfr(h);
+        if (!gp.nw) return;
+        gp.gk0 = (uint32_t)(h0 * F);
+        gp.gfr0 = wfr[(size_t)h0 * F];
+        gp.gcams = cams + (size_t)h0 * F;
     };
     auto launch_group = [&](int g, bool timed) -> rv_status {
         // render part: group g (none in the prologue, g = -1); pre-pass of group g+1; phase A: group g+2
@@ -2152,10 +2159,7 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
         f.nbatch = std::max(gp.nr, 1u);
         gp.rlen1 = pipe_len(f, PIPE_RENDER, 0);
         gp.ov = c->gring; gp.gmask = gmask; gp.cmask = cmask;
-        if (g >= 0) {
-            gp.ov_s = wfirst[(size_t)g * F]; gp.ov_p = wpos[(size_t)g * F];
-            for (uint32_t j = 0; j < gp.nr; j++) gp.ov_len[j] = gsum(g, (int)j + 1);   // frame j sees its own update
-        }
+        if (g >= 0) { gp.ov_s = wfirst[(size_t)g * F]; gp.ov_p = wpos[(size_t)g * F]; }
         const int hp = g + 1;   // the pre-pass's group
         gp.np = (uint32_t)nfr(hp);
         gp.plen1 = pipe_len(f, PIPE_PP, 0);
@@ -2164,8 +2168,10 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
             gp.pp_hdist = c->gsets[hp & 1].hdist; gp.pp_hshadow = c->gsets[hp & 1].hshadow; gp.pp_bs = hbytes;
         }
         gp.rec = xchg ? c->grec_stage : c->grec_all;
+        gp.F = (uint32_t)F; gp.chunk = (uint32_t)chunk;
+        gp.rslot = (uint32_t)(xchg ? (size_t)F * chunk : (size_t)Nrec * F * chunk);
         gp.glen1 = (uint32_t)(((chunk + 63) / 64 + 7) & ~7ull);
-        if (g < 0) { add_phase_a(gp, 0); add_phase_a(gp, 1); } else { add_phase_a(gp, g + 2); }
+        if (g < 0) set_phase_a(gp, 0, 2); else set_phase_a(gp, g + 2, g + 3);
         gp.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
         gp.gi_counters = c->counters + (size_t)ST_GI * NCNT;
         const uint32_t lens[3] = {gp.nw * gp.glen1, gp.np * gp.plen1, gp.nr * gp.rlen1};
@@ -2244,7 +2250,8 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
     for (int g = 0; g < G; g++) {
         if (g >= 1) HIP_TRY(c, hipStreamWaitEvent(S, ev_pb[g & 1], 0));
         if (xchg && g >= 2) HIP_TRY(c, hipStreamWaitEvent(S, ev_gath[g & 1], 0));   // tile buffers of group g-2 sent
-        if (rv_status ls = launch_group(g, nfr(g) == F)) return ls;
+        // timing (rv_timing_stages): the steady-state launches, whose three parts are all full
+        if (rv_status ls = launch_group(g, nfr(g) == F && nfr(g + 1) == F && nfr(g + 2) == F)) return ls;
         HIP_TRY(c, hipEventRecord(ev_rendered, S));
         launch_gi_apply(S, c->gring, c->gi, wfirst[(size_t)g * F], wpos[(size_t)g * F], gsum(g, nfr(g)), gmask, cmask);
         LAUNCH_CHECK(c);

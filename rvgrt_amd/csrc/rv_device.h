@@ -114,6 +114,30 @@ RV_HD uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 RV_HD int imin(int a, int b) { return a < b ? a : b; }
 RV_HD int imax(int a, int b) { return a > b ? a : b; }
 
+// The two powf calls of computeColor -- fog powf(1/2.71828, len * 0.0004f)
+// (src/StateRender.cu:142) and Fresnel powf(1 - ndv, 5) (:85) -- evaluated in
+// double from separately rounded IEEE operations and rounded to float once.
+// A libm powf is only faithful (CUDA's is <= 2 ulp, glibc's and ocml's
+// differ on rare inputs), so the oracle restates these same operations
+// (oracle/rv_oracle.c or_fog / or_pow5): bit-identical on both sides, and
+// within 1 ulp of the correctly rounded value.  ~25 FP64 VALU per pixel.
+RV_HD double det_exp(double t) {           // e^t for t <= 0
+    if (!(t > -800.0)) return t != t ? t : 0.0;
+    const double k = __builtin_rint(t * 0x1.71547652b82fep+0);   // t / ln2
+    const double r = (t - k * 0x1.62e42fee00000p-1) - k * 0x1.a39ef35793c76p-33;
+    double p = 0x1.6124613a86d09p-33;                            // 1/13!
+    p = p * r + 0x1.1eed8eff8d898p-29; p = p * r + 0x1.ae64567f544e4p-26;
+    p = p * r + 0x1.27e4fb7789f5cp-22; p = p * r + 0x1.71de3a556c734p-19;
+    p = p * r + 0x1.a01a01a01a01ap-16; p = p * r + 0x1.a01a01a01a01ap-13;
+    p = p * r + 0x1.6c16c16c16c17p-10; p = p * r + 0x1.1111111111111p-7;
+    p = p * r + 0x1.5555555555555p-5;  p = p * r + 0x1.5555555555555p-3;
+    p = p * r + 0.5; p = p * r + 1.0; p = p * r + 1.0;
+    return __builtin_ldexp(p, (int)k);
+}
+// powf((float)(1.0 / 2.71828), x): ln of that float is -0x1.ffffe96b50b2ep-1
+RV_HD float fog_pow(float x) { return (float)det_exp((double)x * -0x1.ffffe96b50b2ep-1); }
+RV_HD float pow5(float y) { const double d = y, d2 = d * d; return (float)(d2 * d2 * d); }
+
 // (float)b / 255.0f for a byte b, correctly rounded like the IEEE division it
 // replaces (~10 VALU: div_scale x2, rcp, fma x4, div_fmas, div_fixup) with one
 // multiply by the rounded reciprocal and one fma residual correction: exact for

@@ -45,6 +45,9 @@ struct FrameCam {
     float time, jx, jy;
     float cone_k1, cone_k2;  // cone_basis_scales(): 1/|cross(n, c)|, 1/|cross(n, right)| for an axis normal n
     float vp[16], pvp[16];
+    // grouped reference frames (GroupParams): this frame's GI update as this rank computes its phase A
+    // (cells [gi_first, + gi_count)) and the overlay length its render reads the grid through
+    uint32_t gi_first, gi_count, gi_ovlen, gi_pad;
 };
 
 struct FrameParams {
@@ -113,25 +116,24 @@ struct PipeParams {
 // record (GIRec); phase B (k_gi_phase_b, a small kernel per update) combines
 // the record with the grid the update reads.  Updates not yet copied into the
 // grid live in a ring of cells and are read through WorldOv.
-enum { GRP_MAX = 32 };   // windows (GI updates) of one launch's phase A part; frames <= GRP_MAX / 2
 // record: a = kind << 28 | bounce hit cell (28 bits) | lit << 31; b = atlas texel (GR_HIT) or the
 // sky blend t as float bits (GR_MISS)
 enum : uint32_t { GR_SOLID = 0, GR_HIT = 1, GR_HIT_OOB = 2, GR_MISS = 3, GR_MISS_SUN = 4 };
 struct GroupParams {
     uint32_t part[3], len[3];     // as PipeParams: part[i] dispatched i-th over len[i] workgroups
-    // render part: nr frames of rlen1 workgroups; frame j: FrameParams::cams[j], outputs at the
-    // bs_* strides, GI overlay length ov_len[j] (origin ov_s / ov_p shared by the group)
+    // render part: nr frames of rlen1 workgroups; frame j: FrameParams::cams[j] (its camera and
+    // GI overlay length), outputs at the bs_* strides; overlay origin ov_s / ov_p of the group
     uint32_t nr, rlen1;
     const uint32_t* ov; uint32_t ov_s, ov_p, gmask, cmask;
-    uint32_t ov_len[GRP_MAX / 2];
     // pre-pass part: np frames of plen1 workgroups; frame j: camera pcams[j], images + j * pp_bs
     uint32_t np, plen1;
     const FrameCam* pcams;
     float* pp_hdist; float* pp_hshadow; uint64_t pp_bs;
-    // GI record part (phase A): nw windows of glen1 workgroups; window j: GI frame number
-    // g_frame[j], this rank's cells [g_first[j], + g_count[j]) into rec + g_rec[j]
-    uint32_t nw, glen1;
-    uint32_t g_frame[GRP_MAX], g_first[GRP_MAX], g_count[GRP_MAX], g_rec[GRP_MAX];
+    // GI record part (phase A): nw windows of glen1 workgroups, the updates of the call's frames
+    // gk0 .. gk0 + nw - 1 (window j: GI frame number gfr0 + j, this rank's cells from gcams[j]);
+    // frame k's records at rec + (k / F % 3) * rslot + (k % F) * chunk
+    uint32_t nw, glen1, gk0, gfr0, F, rslot, chunk;
+    const FrameCam* gcams;
     uint2* rec;
     unsigned long long* pp_counters;
     unsigned long long* gi_counters;

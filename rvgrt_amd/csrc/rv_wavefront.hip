@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(256) k_wf_water(World w, FrameParams f) {
             rc = sample_sky(rdir, f.sun);
         }
         float ndv = fmaxf(dot(hn, neg(dir)), 0.0f);
-        float fres = 0.08f + (1.0f - 0.08f) * powf(1.0f - ndv, 5.0f);
+        float fres = 0.08f + (1.0f - 0.08f) * pow5(1.0f - ndv);
         f3 col = lerp(V(0.0f, 0.1f, 0.3f), rc, fres);
         f.hsec[p] = make_float4(col.x, col.y, col.z, 0.0f);
         if (STATS) {
@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(256) k_wf_shade(World w, FrameParams f) {
         } else {
             color = sample_sky(ray_dir(f, x, y), f.sun);
         }
-        float fog = hit ? powf((float)(1.0 / 2.71828), length(sub(hpos, f.pos)) * 0.0004f) : 1.0f;
+        float fog = hit ? fog_pow(length(sub(hpos, f.pos)) * 0.0004f) : 1.0f;
         f3 col = add(scale(color, fog), scale(V(0.95f, 0.95f, 1.0f), 1.0f - fog));
         float mvx = 0.0f, mvy = 0.0f, dep = 1.0f;
         if (hit) {   // mat_mul_vec (cumath.cuh:47-54), glm column-major

@@ -61,6 +61,21 @@ def test_gi_sweeps_bit_exact(rv, atlas, oracle_world, oracle):
     r.close()
 
 
+def test_gi_update_zero_rng_state(rv, atlas, oracle_world, oracle):
+    """The cell whose xorshift state idx + frame * 198491317 wraps to 0
+    (tests/test_oracle.py ZERO_SEED_*): the update terminates and agrees
+    with the oracle (a zero state once hung the GPU, 476 frames into a C4 run)."""
+    from test_oracle import ZERO_SEED_CELL, ZERO_SEED_FRAME
+    ow = oracle_world(6, 6, 6, gi_sweeps=1)
+    r = _gpu_world(rv, atlas, 6, 6, 6, gi_sweeps=1)
+    w2 = oracle.OracleWorld(6, 6, 6, atlas=atlas)
+    w2.bits[:] = ow.bits; w2.csdf[:] = ow.csdf; w2.gi[:] = ow.gi
+    w2.gi_update(ZERO_SEED_FRAME, first=ZERO_SEED_CELL - 40, count=80)
+    r.gi_update(ZERO_SEED_FRAME, first=ZERO_SEED_CELL - 40, count=80)
+    assert np.array_equal(r.world_export(rv.RV_WORLD_GI), w2.gi)
+    r.close()
+
+
 def test_import_export_roundtrip(rv, atlas, oracle_world):
     ow = oracle_world(6, 6, 6, gi_sweeps=1)
     r = rv.StateRender((6, 6, 6), 64, 64, atlas=atlas)

@@ -9,6 +9,7 @@ for step in "$@"; do
     case $step in
         tests) run gtests 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
                    tests/test_gpu_group.py tests/test_gpu_multirank.py "tests/test_gpu_fullsize.py::test_fullsize_pipelined_frames" || exit 3 ;;
+        all) run gall 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/ || exit 3 ;;
         bench) for cfg in ${BENCH_CFGS:-c3 c4}; do for g in ${GROUPS_:-0 4 8}; do
                    run b_${cfg}_g$g 300 python bench.py --config $cfg --group $g --cpu-seconds 0 || exit 3
                    grep -o '"ms_per_step": [0-9.]*\|"frac": [0-9.]*\|"avg_launch_ms": [0-9.]*' gpurun_out/b_${cfg}_g$g.log | tr '\n' ' '; echo

@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 
 
 def per_frame_us(r, cam, vp, frames, gi, reps=3):
+    print(f"  [{time.strftime('%X')}] {frames} frames ...", flush=True)
     r.render_frames(frames, cam, vp, gi_per_frame=gi)      # warm: tile lists, cost order
     r.sync()
     best = 1e30
@@ -32,6 +33,8 @@ def per_frame_us(r, cam, vp, frames, gi, reps=3):
 
 
 def main():
+    import faulthandler
+    faulthandler.dump_traceback_later(45, repeat=True)   # a stuck call names itself
     import rvgrt_amd as rv
     from rvgrt_amd.atlas import load_atlas
     from rvgrt_amd.configs import CONFIGS, pose_f32
