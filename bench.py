@@ -32,11 +32,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-# Scattered-gather ceiling of the vector L1 / texture path, measured with
-# tools/ubench/gather.hip (profiles/r01_ubench_gather.txt): once a wave's
-# lanes fall in >= 16 lines an L1-resident dword gather costs ~1 cycle per
-# lane per CU -> 256 CUs x 2.4 GHz lane-gathers/s.
-GATHER_CEILING = 256 * 2.4e9
 
 
 def log(*a):
@@ -188,7 +183,11 @@ def main():
     streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.stream_priority) for _ in range(nfl - 1)]
     r.set_gi_async(args.gi_async)
     r.set_pipeline(args.pipe)
-    group = args.group if args.group is not None else 0
+    # grouped reference frames by default from 4 ranks on (tools/shard_probe.py, profiles/r03/, 64-px tiles:
+    # the slowest C4 rank share at 8 ranks 163.5 -> 93.2 -> 87.7 us/frame with 8 / 16 frames per launch,
+    # C5 198.1 -> 122.0 -> 114.1; at 4 ranks C4 182.4 -> 162.0 at 16; at 2 ranks 278.9 -> 307.5 and on one
+    # GPU 508 -> 561, so those keep the per-frame pipeline; the library caps the group by the GI grid)
+    group = args.group if args.group is not None else (16 if world_size >= 4 else 0)
     r.set_frame_group(group)
     t0 = time.perf_counter()
     r.world_build()
@@ -484,7 +483,8 @@ def main():
         dom_bytes = dom_bytes * len(my_tiles) / ntiles
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}" + ("" if args.pose == "P0" else f"_{args.pose}")
+                         + ".json")
     if os.path.exists(tpath) and world_size == 1:   # PMC summaries are of the one-GPU launch
         try:
             tj = json.load(open(tpath))
@@ -504,11 +504,15 @@ def main():
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
                 "avg_launch_ms": round(dom_ms, 4), "frames_per_launch": dom_fpl,
-                # the limit that binds in practice: traversal gathers per second
-                # against the scattered-gather ceiling of the L1/texture path
+                # measured HBM bytes (PMC, profiles/traffic_<config>.json) per launch time against the peak:
+                # the memory side's real load, beside frac's algorithmic bytes
+                "traffic_frac": (round(traffic / (dom_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+                                 if traffic and dom_ms > 0 else None),
+                # what binds in practice: traversal gathers per second through the vector
+                # L1 / texture path (no ceiling is claimed: coherent gathers cost less than the
+                # scattered-gather micro-benchmark's ~1 lane per CU-cycle, so C2 runs above it)
                 "gathers_per_launch": int(gathers), "gather_rate": round(gather_rate / 1e9, 2),
-                "gather_ceiling": round(GATHER_CEILING / 1e9, 1), "gather_unit": "G lane-gathers/s",
-                "gather_frac": round(gather_rate / GATHER_CEILING, 4)}
+                "gather_unit": "G lane-gathers/s"}
 
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
@@ -517,7 +521,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": f"Mrays/s ({cfg.name}: {cfg.describe})",
+            "metric": f"Mrays/s ({cfg.name}: {cfg.describe}, pose {args.pose}, "
+                      + (f"screen-tile split x{world_size} (RCCL gather))" if world_size > 1 else "1 GPU)"),
             "value": round(mrays, 2),
             "unit": "Mrays/s",
             "n_gpus": world_size,

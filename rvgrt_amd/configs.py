@@ -45,9 +45,9 @@ CONFIGS = {
     "c3": RenderConfig("c3", 10, 1920, 1080, FLAGS_REFERENCE, 1, True, 1,
                        "1024^3 world, 1920x1080, 1-bounce reflection + voxel-cone GI"),
     "c4": RenderConfig("c4", 10, 3840, 2160, FLAGS_REFERENCE, 2, True, 4,
-                       "1024^3 world, 3840x2160, 2-bounce GI, screen-tile split (RCCL gather)"),
+                       "1024^3 world, 3840x2160, 2-bounce GI"),
     "c5": RenderConfig("c5", 11, 3840, 2160, FLAGS_REFERENCE, 2, True, 8,
-                       "2048^3 world, 3840x2160, 2-bounce GI + reflections, tile-parallel"),
+                       "2048^3 world, 3840x2160, 2-bounce GI + reflections"),
 }
 
 # Poses for the small (128^3) parity worlds: the C1-C5 pose rule puts the

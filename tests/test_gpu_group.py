@@ -112,3 +112,31 @@ def test_grouped_frames_512_world_default_window(rv, atlas):
     assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ref.world_export(rv.RV_WORLD_GI))
     r.close()
     ref.close()
+
+
+def test_grouped_frames_one_rank_rccl(rv, atlas):
+    """Grouped reference frames through a one-rank RCCL communicator (the
+    transport bench.py uses at N >= 4: sharded phase A, the record all-gather
+    per group, the tile gather to rank 0 and its assembly) equal one context
+    rendering whole frames one at a time."""
+    from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    lg, W, H, rays = 7, 320, 192, 2048
+    flags = rv.RV_FLAGS_REFERENCE
+    seq = camera_path(TEST_POSES_128["P0"], W, H, 16, pan=0.01, ref_compat=True)
+    ref, r = _make(rv, atlas, lg, W, H, rays), _make(rv, atlas, lg, W, H, rays)
+    ref.set_pipeline(0)
+    r.set_tile_shard(64, 0, 1)
+    r.set_gather_bpp(3)
+    r.set_frame_group(8)
+    comm = rv.Comm(r, rv.Comm.unique_id(), 1, 0)
+    k = 0
+    for n in (9, 6):
+        r.render_frame_seq(seq[k:k + n], next_desc=seq[k + n], flags=flags, gi_per_frame=True, comm=comm)
+        for d in seq[k:k + n]:
+            _ref_step(rv, ref, d, flags)
+        k += n
+        assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref.readback(rv.RV_IMAGE_COLOR)), n
+        assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ref.world_export(rv.RV_WORLD_GI)), n
+    comm.close()
+    r.close()
+    ref.close()
