@@ -183,11 +183,17 @@ def main():
     streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.stream_priority) for _ in range(nfl - 1)]
     r.set_gi_async(args.gi_async)
     r.set_pipeline(args.pipe)
-    # grouped reference frames by default from 4 ranks on (tools/shard_probe.py, profiles/r03/, 64-px tiles:
-    # the slowest C4 rank share at 8 ranks 163.5 -> 93.2 -> 87.7 us/frame with 8 / 16 frames per launch,
-    # C5 198.1 -> 122.0 -> 114.1; at 4 ranks C4 182.4 -> 162.0 at 16; at 2 ranks 278.9 -> 307.5 and on one
-    # GPU 508 -> 561, so those keep the per-frame pipeline; the library caps the group by the GI grid)
-    group = args.group if args.group is not None else (16 if world_size >= 4 else 0)
+    # Grouped reference frames (rv_set_frame_group) when a rank's render part is latency-bound (<= 48 K
+    # waves of 64 pixels, as the latency-mode pipelined variant): the group's frames share one tail.
+    # tools/shard_probe.py / tools/r03_ab.sh (profiles/r03/), 64-px tiles: C3 on one GPU 0.2234 -> 0.2063 ms
+    # at 8 frames per launch (0.2089 at 16); the slowest C4 rank share at 8 ranks 163.5 -> 93.2 -> 87.7 us/frame
+    # at 8 / 16, C5 198.1 -> 122.0 -> 114.1, at 4 ranks C4 182.4 -> 162.0 at 16.  Throughput-bound launches
+    # keep the per-frame pipeline: C4 one GPU 0.491 -> 0.553 ms at 16, a 2-rank C4 share 278.9 -> 307.5 us.
+    # The library caps the group by the GI grid (two groups' updates never overlap).
+    rank_waves = (W * H // 64) // max(world_size, 1)
+    group = args.group if args.group is not None else \
+        ((8 if world_size == 1 else 16) if gi_per_frame and prepass and args.pipe and args.path == "fused"
+         and rank_waves <= 49152 else 0)
     r.set_frame_group(group)
     t0 = time.perf_counter()
     r.world_build()
@@ -205,7 +211,7 @@ def main():
     # frames the run takes from the path: warm-up, timed, the stage-timing pass, 9 latency frames
     n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if nfl > 1 else min(args.steps, 10)
     if group >= 2:   # whole groups: the timing pass records only full-group launches
-        n_stage_frames = group * max(2, min(args.steps // group, 6))
+        n_stage_frames = group * max(3, min(args.steps // group, 6))
     n_path = args.warmup + args.steps + n_stage_frames + 9 + 2
     pan = args.pan if args.camera == "path" else 0.0
     path = camera_path((pos, yaw, pitch), W, H, n_path, pan=pan, ref_compat=args.camera == "path")
@@ -409,8 +415,8 @@ def main():
     stage_fpl = {name: fpl for name in rv._lib.STAGES}
     if gi_groups:
         stage_fpl["pp_primary"] = nfl
-    if not grouped:
-        n_stage_frames = min(args.steps, 10)
+    if not grouped and ref_group < 2:   # (grouped reference frames keep whole groups: only launches whose
+        n_stage_frames = min(args.steps, 10)   # three parts are all full are timed)
     serial[0] = True
     r.timing_enable(2 * n_stage_frames + 2)
     if native:

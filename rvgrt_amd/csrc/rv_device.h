@@ -422,25 +422,40 @@ RV_HD bool tile_has(const WorldTile& w, uint32_t bx, uint32_t by, uint32_t bz, u
     q = (((k << 1) | j) << 1) | i;
     return (i | j | k) < 2u;
 }
+// RV_TILE_UNIFORM (round 3): the choice between the tile and the world is made per wave, not per
+// lane -- a gather whose active lanes all fall inside the tile reads LDS and issues no vector-memory
+// instruction (a scalar branch on the ballot); any lane outside sends the whole wave to the world.
+// Per-lane selection (round 2, 0) still issued the global load for the lanes outside and cost VALU
+// +8 % (profiles/r02/lds_tile_ab.txt).
+#ifndef RV_TILE_UNIFORM
+#define RV_TILE_UNIFORM 1
+#endif
+RV_HD bool tile_use(bool in) {
+#if RV_TILE_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(!in) == 0;
+#else
+    return in;
+#endif
+}
 RV_HD uint32_t voxel_word_at(const WorldTile& w, uint32_t x, uint32_t y, uint32_t z) {
     uint32_t q;
-    if (tile_has(w, x >> 3, y >> 3, z >> 3, q)) return w.tile[q * 16u + (((y >> 2) & 1u) | ((z & 7u) << 1))];
+    if (tile_use(tile_has(w, x >> 3, y >> 3, z >> 3, q))) return w.tile[q * 16u + (((y >> 2) & 1u) | ((z & 7u) << 1))];
     return voxel_load(w, voxel_word_off(w, x, y, z));
 }
 RV_HD uint32_t csdf_word_at(const WorldTile& w, uint32_t cx, uint32_t cy, uint32_t cz) {
     uint32_t q;
-    if (tile_has(w, cx >> 2, cy >> 2, cz >> 2, q))
+    if (tile_use(tile_has(w, cx >> 2, cy >> 2, cz >> 2, q)))
         return w.tile[128u + q * 16u + (((cy & 3u) >> 0) | ((cz & 3u) << 2))];
     return csdf_load(w, csdf_off(w, cx, cy, cz));
 }
 RV_HD uint32_t voxel_word_nc(const WorldTile& w, uint32_t x, uint32_t y, uint32_t z) {
     uint32_t q;
-    if (tile_has(w, x >> 3, y >> 3, z >> 3, q)) return w.tile[q * 16u + (((y >> 2) & 1u) | ((z & 7u) << 1))];
+    if (tile_use(tile_has(w, x >> 3, y >> 3, z >> 3, q))) return w.tile[q * 16u + (((y >> 2) & 1u) | ((z & 7u) << 1))];
     return voxel_word_nc(static_cast<const World&>(w), x, y, z);
 }
 RV_HD uint32_t csdf_step_byte(const WorldTile& w, uint32_t fx, uint32_t fy, uint32_t fz) {
     uint32_t q;
-    if (tile_has(w, fx >> 3, fy >> 3, fz >> 3, q))
+    if (tile_use(tile_has(w, fx >> 3, fy >> 3, fz >> 3, q)))
         return csdf_byte(w.tile[128u + q * 16u + (((fy >> 1) & 3u) | (((fz >> 1) & 3u) << 2))], fx >> 1);
     return csdf_step_byte(static_cast<const World&>(w), fx, fy, fz);
 }

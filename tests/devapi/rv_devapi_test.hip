@@ -5,6 +5,7 @@
 // Built for a 128 x 64 x 128 world (RVGRT_SHIX/Y/Z from the Makefile).
 // Test infrastructure: nothing in the product links it.
 #include "../../include/rvgrt_device.h"
+#include "../../include/rvgrt_kernels.h"
 
 #include <vector>
 
@@ -188,6 +189,43 @@ int rvt_lookup(const uint32_t* bits, size_t nbits, const uint8_t* csdf, size_t n
     d.down(solid, s, 4ull * n);
     d.down(di, x, 4ull * n);
     d.down(df, y, 4ull * n);
+    return (int)d.err;
+}
+
+// drawCUDA's sequence (src/StateRender.cu:289-346) through the reference-signature kernels of
+// include/rvgrt_kernels.h: the three constant uploads, distApproximationKernel over W/2 x H/2 and
+// renderKernel over W x H in 8 x 8 blocks, into pitched outputs (pitch = row + 192 B).  Returns
+// the images row-packed: colour W*H*4, motion W*H*4, depth W*H*2, half distance / shadow.
+int rvt_frame(const uint32_t* bits, size_t nbits, const uint8_t* csdf, size_t ncsdf, const uint8_t* gi, size_t ngi,
+              const uint32_t* atlas, int aw, int ah, const float* cam18, const float* vp, const float* pvp, int W,
+              int H, uint8_t* color, uint8_t* mv, uint8_t* depth, float* hdist, float* hshadow) {
+    if (W <= 0 || H <= 0 || (W & 1) || (H & 1)) return -1;
+    const int hw = W / 2, hh = H / 2;
+    const size_t pc = 4ull * W + 192, pm = 4ull * W + 192, pd = 2ull * W + 192;
+    Dev d;
+    auto* b = d.up<uint32_t>(bits, nbits);
+    auto* c = d.up<unsigned char>(csdf, ncsdf);
+    auto* g = d.up<uchar4>(gi, ngi);
+    rvgrtAtlas at{d.up<uint32_t>(atlas, 4ull * aw * ah), aw, ah};
+    auto* fb = d.up<uchar4>(nullptr, pc * H);
+    auto* m = d.up<__half2>(nullptr, pm * H);
+    auto* z = d.up<__half>(nullptr, pd * H);
+    auto* hd = d.up<float>(nullptr, 4ull * hw * hh);
+    auto* hs = d.up<float>(nullptr, 4ull * hw * hh);
+    if (d.err == hipSuccess) d.err = rvgrtUploadFrameConstants(cam18, vp, pvp, 0);
+    const dim3 block(8, 8);
+    if (d.err == hipSuccess)
+        hipLaunchKernelGGL(distApproximationKernel, dim3((hw + 7) / 8, (hh + 7) / 8), block, 0, 0,
+                           rvgrtFloatSurf{hd, hw, hh}, rvgrtFloatSurf{hs, hw, hh}, hw, hh, b, c);
+    if (d.err == hipSuccess)
+        hipLaunchKernelGGL(renderKernel, dim3((W + 7) / 8, (H + 7) / 8), block, 0, 0, fb, m, z,
+                           rvgrtFloatTex{hd, hw, hh}, rvgrtFloatTex{hs, hw, hh}, pc, pm, pd, W, H, b, c, g, at);
+    d.launched();
+    if (d.err == hipSuccess) d.err = hipMemcpy2D(color, 4ull * W, fb, pc, 4ull * W, H, hipMemcpyDeviceToHost);
+    if (d.err == hipSuccess) d.err = hipMemcpy2D(mv, 4ull * W, m, pm, 4ull * W, H, hipMemcpyDeviceToHost);
+    if (d.err == hipSuccess) d.err = hipMemcpy2D(depth, 2ull * W, z, pd, 2ull * W, H, hipMemcpyDeviceToHost);
+    d.down(hdist, hd, 4ull * hw * hh);
+    d.down(hshadow, hs, 4ull * hw * hh);
     return (int)d.err;
 }
 

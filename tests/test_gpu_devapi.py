@@ -32,7 +32,8 @@ def load():
     if not os.path.exists(LIB):
         raise RuntimeError(f"{LIB} missing: run __graft_entry__.build()")
     L = C.CDLL(LIB)
-    for name in ("rvt_trace", "rvt_approx", "rvt_cone", "rvt_texture", "rvt_sky", "rvt_lookup", "rvt_dims"):
+    for name in ("rvt_trace", "rvt_approx", "rvt_cone", "rvt_texture", "rvt_sky", "rvt_lookup", "rvt_dims",
+                 "rvt_frame"):
         getattr(L, name).restype = C.c_int
     return L
 
@@ -157,3 +158,50 @@ def test_devapi_issolid_getdistance(world):
     assert np.array_equal(di, cs[c[:, 2], c[:, 1], c[:, 0]].astype(np.int32))
     c = np.clip(np.trunc(np.floor(fp) * np.float32(0.5)).astype(np.int64), 0, S - 1)
     assert np.array_equal(df, cs[c[:, 2], c[:, 1], c[:, 0]].astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pose", ["land", "water"])
+def test_devapi_reference_kernels_frame(world, oracle, atlas, pose):
+    """renderKernel / distApproximationKernel with the reference's argument
+    lists (include/rvgrt_kernels.h; src/StateRender.cu:200-286), launched as
+    drawCUDA launches them after its three constant uploads, into pitched
+    outputs: the frame (RGBA8, motion vectors, depth) and the half-res images
+    equal the oracle's bit for bit -- with drawCUDA's c_cam layout, so time =
+    the uploaded jitterY and jitter (0, 0) (Appendix R1), and minDist's
+    reference texel fetch (RV_F_REF_FETCH)."""
+    import rvgrt_amd as rv
+    L = load()
+    W, H = 192, 128
+    if pose == "land":
+        pos, yaw, pitch = (100.0, 50.0, 110.0), 2.44, -3.4415927
+    else:
+        pos, yaw, pitch = (64.0, 40.0, 120.0), 3.14, -3.2
+    cam, vp = rv.camera_from_pose(pos, np.float32(yaw), np.float32(pitch), W, H)
+    _, pvp = rv.camera_from_pose((pos[0] + 0.5, pos[1], pos[2]), np.float32(yaw + 0.01), np.float32(pitch), W, H)
+    d = rv.camera_dict(cam, vp)
+    sun = oracle.sun_dir()
+    t_up, jx_up, jy_up = 5.25, 0.0007, 0.37   # what drawCUDA packs as time, jitterX, jitterY
+    cam18 = np.array([*d["pos"], *d["fo"], *d["ri"], *d["up"], *sun, t_up, jx_up, jy_up], np.float32)
+    vpa, pvpa = np.ascontiguousarray(vp, np.float32).ravel(), np.ascontiguousarray(pvp, np.float32).ravel()
+    at = np.ascontiguousarray(atlas)
+    color = np.zeros((H, W, 4), np.uint8)
+    mv = np.zeros((H, W, 2), np.uint16)
+    depth = np.zeros((H, W), np.uint16)
+    hd = np.zeros((H // 2, W // 2), np.float32)
+    hs = np.zeros_like(hd)
+    rc = L.rvt_frame(_p(world.bits), C.c_size_t(world.bits.nbytes), _p(world.csdf), C.c_size_t(world.csdf.nbytes),
+                     _p(world.gi), C.c_size_t(world.gi.nbytes), _p(at), at.shape[1], at.shape[0], _p(cam18),
+                     _p(vpa), _p(pvpa), W, H, _p(color), _p(mv), _p(depth), _p(hd), _p(hs))
+    assert rc == 0, f"hip error {rc}"
+    ow = oracle.OracleWorld(*DIMS, atlas=at)
+    ow.bits[:] = world.bits
+    ow.csdf[:] = world.csdf
+    ow.gi[:] = world.gi
+    fr = oracle.make_frame(W, H, rv.RV_FLAGS_REFERENCE | rv.RV_F_REF_FETCH, d, time=jy_up, jx=0.0, jy=0.0, pvp=pvpa)
+    ref = oracle.render(ow, fr, want_stats=False)
+    assert np.array_equal(hd.view(np.uint32), ref["halfdist"].view(np.uint32))
+    assert np.array_equal(hs, ref["halfshadow"])
+    assert np.array_equal(color, ref["rgba"])
+    assert np.array_equal(mv, ref["mv"]) and np.array_equal(depth, ref["depth"])
+    assert len(np.unique(color.reshape(-1, 4), axis=0)) > 50 and (mv != 0).any()
