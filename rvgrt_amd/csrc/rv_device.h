@@ -408,8 +408,14 @@ struct WorldOv : World {
     const uint32_t* __restrict__ ov;
     uint32_t ov_s, ov_p, ov_len, gmask, cmask;
 };
+// RV_OV_SELECT: one gather per texel from a per-lane address select (the two-load form may issue
+// a gather into each buffer under complementary exec masks).
+#ifndef RV_OV_SELECT
+#define RV_OV_SELECT 0
+#endif
 RV_HD uint32_t gi_texel(const WorldOv& w, uint32_t idx) {
     const uint32_t off = (idx - w.ov_s) & w.gmask;
+    if (RV_OV_SELECT) return *(off < w.ov_len ? w.ov + ((w.ov_p + off) & w.cmask) : w.gi + idx);
     return off < w.ov_len ? w.ov[(w.ov_p + off) & w.cmask] : w.gi[idx];
 }
 

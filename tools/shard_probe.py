@@ -61,7 +61,7 @@ def main():
     full = per_frame_us(r, cam, vp, frames, gi)
     print(f"{cfg.name}: whole frame {full:.1f} us/frame at K={K}", flush=True)
     for T in sizes:
-        for N in (2, 4, 8):
+        for N in [int(v) for v in os.environ.get("SHARD_NS", "2,4,8").split(",")]:
             t = []
             for rank in range(N):
                 r.set_tile_shard(T, rank, N)
