@@ -30,10 +30,14 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--fpl", type=int, default=8, help="frames per launch of the profiled bench run")
     ap.add_argument("--prefix", default="", help="pass directories pmc_<prefix>* only (gpu_run.sh PMC_TAG)")
-    ap.add_argument("--grid", type=int, default=0, help="dispatches of this Grid_Size only (e.g. the full-group launches)")
+    ap.add_argument("--grid", type=int, default=0, help="dispatches of this Grid_Size only (-1: the largest, i.e. the full-group launches)")
     a = ap.parse_args()
     vals = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(a.dir, f"pmc_{a.prefix}*", "*counter_collection.csv")):
+    files = glob.glob(os.path.join(a.dir, f"pmc_{a.prefix}*", "*counter_collection.csv"))
+    if a.grid < 0:   # the largest grid of the kernel: the full-group launches of a grouped loop
+        a.grid = max(int(row.get("Grid_Size", 0)) for f in files for row in csv.DictReader(open(f))
+                     if a.kernel in row["Kernel_Name"])
+    for f in files:
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
             if a.kernel not in name or (a.grid and int(row.get("Grid_Size", 0)) != a.grid):
@@ -44,7 +48,7 @@ def main():
         raise SystemExit("no FETCH_SIZE rows for " + a.kernel)
     read_b = 2.0 * avg["FETCH_SIZE"] * 1024
     write_b = avg.get("WRITE_SIZE", 0.0) * 1024
-    out = {"kernel": a.kernel, "config": a.config, "frames_per_launch": a.fpl,
+    out = {"kernel": a.kernel, "config": a.config, "frames_per_launch": a.fpl, "launches": len(vals.get("FETCH_SIZE", [])),
            "hbm_bytes_per_launch": int(read_b + write_b),
            "read_bytes_per_launch": int(read_b), "write_bytes_per_launch": int(write_b),
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 64-B tally of 128-B requests), write = WRITE_SIZE KiB",
