@@ -74,6 +74,7 @@ struct rv_ctx {
     rv_config cfg{};
     int lx = 0, ly = 0, lz = 0;
     World w{};
+    uint32_t* d_top = nullptr;     // world_top scratch (one dword)
     uint32_t* brick = nullptr;
     size_t brick_bytes = 0;
     uint32_t* gi = nullptr;       // current grid
@@ -453,6 +454,7 @@ void rv_destroy(rv_ctx* c) {
     if (!c->slots.empty()) slot_save(c);
     for (FrameSlot& sl : c->slots) slot_free(sl);
     hipFree(c->counters);
+    hipFree(c->d_top);
     hipFree(c->tiles.d); hipFree(c->untile_ids.d);
     hipFree(c->tilebuf);
     hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
@@ -631,6 +633,23 @@ rv_status rv_sync(rv_ctx* c) {
     return RV_OK;
 }
 
+// The sky exit of the frame traversal (World::ytop, rv_device.h trace): the highest solid voxel
+// row + 2, recomputed after every write of the bits.  Env RV_SKY_EXIT=0 turns it off (ytop = Y).
+static rv_status world_top(rv_ctx* c) {
+    c->w.ytop = (uint32_t)c->w.Y;
+    const char* e = getenv("RV_SKY_EXIT");
+    if (e && e[0] == '0') return RV_OK;
+    if (!c->d_top) HIP_TRY(c, hipMalloc(&c->d_top, 4));
+    HIP_TRY(c, hipMemsetAsync(c->d_top, 0, 4, c->stream));
+    launch_world_top(c->stream, c->brick, current_world(c), c->d_top);
+    LAUNCH_CHECK(c);
+    uint32_t top = 0;
+    HIP_TRY(c, hipMemcpyAsync(&top, c->d_top, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->w.ytop = std::min((uint32_t)c->w.Y, top + 1u);   // top = max solid y + 1
+    return RV_OK;
+}
+
 rv_status rv_csdf_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
@@ -667,6 +686,7 @@ rv_status rv_world_build(rv_ctx* c) {
     c->geom_ver++;
     launch_fill_bricks(c->stream, c->brick, current_world(c), c->cfg.seed_x, c->cfg.seed_z);
     LAUNCH_CHECK(c);
+    if (rv_status ts = world_top(c)) return ts;
     rv_status s = rv_csdf_build(c);
     if (s != RV_OK) return s;
     s = rv_gi_init(c);
@@ -688,6 +708,7 @@ rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t byte
         LAUNCH_CHECK(c);
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         hipFree(d);
+        if (rv_status ts = world_top(c)) return ts;
     } else if (kind == RV_WORLD_CSDF) {
         if (bytes != n_csdf(c)) return fail(c, RV_ERR_INVALID, "csdf size mismatch");
         uint8_t* d = nullptr;
@@ -1262,7 +1283,9 @@ rv_status rv_trace_rays(rv_ctx* c, const float* org, const float* dir, const flo
     HIP_TRY(c, hipMemcpyAsync(d_o, org, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(d_d, dir, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(d_t, dist, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-    launch_trace_rays(c->stream, current_world(c), d_o, d_d, d_t, n, d_h);
+    World tw = current_world(c);
+    tw.ytop = (uint32_t)tw.Y;   // rv_trace_rays reports the reference's step counts: no sky exit
+    launch_trace_rays(c->stream, tw, d_o, d_d, d_t, n, d_h);
     LAUNCH_CHECK(c);
     HIP_TRY(c, hipMemcpyAsync(out, d_h, (size_t)n * sizeof(RvHitDev), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));

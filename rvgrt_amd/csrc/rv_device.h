@@ -171,6 +171,7 @@ struct World {
     int aw, ah;
     uint32_t coff;                       // byte offset of brick 0's 64 CSDF bytes
     uint32_t omax;                       // last dword offset valid in both regions (world_set_regions)
+    uint32_t ytop;                       // sky exit (trace): max solid y + 2, or Y (no exit)
     const uint32_t* __restrict__ csdf;   // = brick + coff: the CSDF region's own base, so a CSDF
                                          // gather is SGPR base + the brick-relative offset
 };
@@ -199,6 +200,7 @@ __host__ __device__ inline uint32_t csdf_region(uint64_t nbricks) { return RV_SP
 // offset that is valid from both region bases (the unclamped traversal gathers clamp to it).
 __host__ __device__ inline void world_set_regions(World& w, uint64_t nbricks) {
     w.coff = csdf_region(nbricks);
+    w.ytop = (uint32_t)w.Y;   // no sky exit until the world's top is known (world_top_y)
     w.omax = (uint32_t)(nbricks * (RV_SPLIT_BRICKS ? 64u : 128u) - (RV_SPLIT_BRICKS ? 4u : 68u));
 }
 // dword index of bit word wd (0..15) / byte index of CSDF byte `local` of brick b
@@ -246,6 +248,18 @@ RV_HD bool is_solid(const World& w, int x, int y, int z) {
     return (word >> voxel_bit((uint32_t)x, (uint32_t)y)) & 1u;
 }
 
+// Highest solid row of a brick's 16 bit dwords + 1 (0: empty brick); by = the brick's y index.
+// Dword d holds rows y = (d & 1) * 4 + 0..3 of one z slice, row (y & 3) in bits 8 (y & 3) .. +7.
+RV_HD uint32_t brick_top_y(const uint32_t* wd, uint32_t by) {
+    uint32_t t = 0;
+    for (uint32_t d = 0; d < 16; d++)
+        if (wd[d]) {
+            const uint32_t y = by * 8u + ((d & 1u) << 2) + ((31u - (uint32_t)__builtin_clz(wd[d])) >> 3);
+            t = t > y + 1u ? t : y + 1u;
+        }
+    return t;
+}
+
 // CSDF byte of an in-range coarse cell: the dword holding it, then the byte
 // (4x4x4 cells per record, byte = (cx&3) | (cy&3)<<2 | (cz&3)<<4 after 64 B of bits).
 // byte offset from World::csdf
@@ -283,6 +297,7 @@ struct LinearWorld {
     int SX, SY, SZ;
     int GX, GY, GZ;
     int aw, ah;
+    uint32_t ytop;                       // = Y: the reference-layout API keeps the reference's step counts
 };
 RV_HD LinearWorld linear_world(int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf,
                                const uint32_t* gi = nullptr, const uint32_t* atlas = nullptr, int aw = 256,
@@ -294,6 +309,7 @@ RV_HD LinearWorld linear_world(int lx, int ly, int lz, const uint32_t* bits, con
     w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
     w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
     w.aw = aw; w.ah = ah;
+    w.ytop = (uint32_t)w.Y;
     return w;
 }
 RV_HD uint32_t csdf_off(const LinearWorld& w, uint32_t cx, uint32_t cy, uint32_t cz) {
@@ -684,6 +700,9 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     const int sy = (dir.y > 0) - (dir.y < 0);
     const int sz = (dir.z > 0) - (dir.z < 0);
     const uint32_t X = (uint32_t)w.X, Y = (uint32_t)w.Y, Z = (uint32_t)w.Z;
+    // Sky exit: a ray that does not descend (dir.y >= 0) and has risen to y >= w.ytop (the highest
+    // solid voxel row + 2; Y when unset) can only miss, so it "leaves the grid" there (World::ytop).
+    const uint32_t YL = sy >= 0 ? umin(Y, w.ytop) : Y;
     int ix = 0, iy = 0, iz = 0, mask = -128;
     float tx = 0.0f, ty = 0.0f, tz = 0.0f;
     int status = 0;   // 0: gave up (miss), 2: left the grid (miss), 3: hit
@@ -696,7 +715,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         bool oob = false;
         for (int it = 0; it < 100; it++) {
             const int fx = floor_i(cur.x), fy = floor_i(cur.y), fz = floor_i(cur.z);
-            oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= Y) | ((uint32_t)fz >= Z);
+            oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= YL) | ((uint32_t)fz >= Z);
             uint32_t d;
             if (REUSE) {   // gather only where the CSDF dword changed
                 const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
@@ -763,7 +782,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
 #pragma unroll
             for (int j = 0; j < G; j++) {
                 if (j == 0 || j == G - 1)
-                    ob_ends = ob_ends | ((uint32_t)jx >= X) | ((uint32_t)jy >= Y) | ((uint32_t)jz >= Z);
+                    ob_ends = ob_ends | ((uint32_t)jx >= X) | ((uint32_t)jy >= YL) | ((uint32_t)jz >= Z);
                 RV_GD(gd::DDA, voxel_ptr(w, voxel_word_off(w, umin((uint32_t)jx, X - 1u), umin((uint32_t)jy, Y - 1u),
                                                            umin((uint32_t)jz, Z - 1u))));
                 wv[j] = voxel_word_nc(w, (uint32_t)jx, (uint32_t)jy, (uint32_t)jz);   // unused outside
@@ -795,7 +814,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 float vx = tx, vy = ty, vz = tz;
 #pragma unroll
                 for (int j = 0; j < G; j++) {
-                    const bool ob = ((uint32_t)qx >= X) | ((uint32_t)qy >= Y) | ((uint32_t)qz >= Z);
+                    const bool ob = ((uint32_t)qx >= X) | ((uint32_t)qy >= YL) | ((uint32_t)qz >= Z);
                     sm |= ob ? 1u << j : 0u;
                     const bool cxy = vx < vy, cxz = vx < vz, cyz = vy < vz;
                     const bool selx = cxy & cxz, sely = !cxy & cyz, selz = !(cxy & cxz) & !(!cxy & cyz);
@@ -835,7 +854,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 iz += selz ? sz : 0;
                 mask = go ? (selx ? 0 : (sely ? 1 : 2)) : mask;
             }
-            const bool ob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
+            const bool ob = ((uint32_t)ix >= X) | ((uint32_t)iy >= YL) | ((uint32_t)iz >= Z);
             st = jmp ? 1 : (ob ? 2 : 3);
             if (COUNT) sc.dda += st == 3 ? 1u : 0u;
         }
@@ -882,7 +901,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                     if (COUNT) sc.check++;
                     st = jd > 2 ? 1 : 0;
                 }
-                const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
+                const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= YL) | ((uint32_t)iz >= Z);
                 const bool solid = (wv[j] >> voxel_bit(w, (uint32_t)ix, (uint32_t)iy)) & 1u;
                 if (COUNT) sc.dda += (st == 0) & !oob;
                 st = st != 0 ? st : (oob ? 2 : (solid ? 3 : 0));
@@ -913,7 +932,7 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
                 if (COUNT) sc.check++;
                 st = jd > 2 ? 1 : 0;
             }
-            const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= Y) | ((uint32_t)iz >= Z);
+            const bool oob = ((uint32_t)ix >= X) | ((uint32_t)iy >= YL) | ((uint32_t)iz >= Z);
             // always-valid gather; its bit only counts in bounds
             uint32_t word;
             if (REUSE) {   // a word covers 8 (x) x 4 (y) voxels: runs along x/y re-read it

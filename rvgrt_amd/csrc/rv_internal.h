@@ -157,6 +157,8 @@ void launch_gi_update(hipStream_t s, const uint32_t* prev, uint32_t* next, const
                       bool stats = false);
 // workgroups of the kernel that fills queue q (sizes its per-XCD sub-queues)
 uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
+// the world's highest solid row + 1 into *top (device, pre-zeroed): World::ytop = it + 1
+void launch_world_top(hipStream_t s, const uint32_t* brick, const World& w, uint32_t* top);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);
 void launch_render(hipStream_t s, const World& w, const FrameParams& f);
 // workgroups of each part of a pipelined launch; then the launch itself

@@ -49,6 +49,20 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
             }
     world_set_brick(w, h.brick.data());
 }
+// World::ytop as rv_abi.cpp's world_top sets it: highest solid row + 2, at most Y
+uint32_t world_ytop(const HostWorld& h) {
+    const World& w = h.w;
+    const uint64_t nb = ((uint64_t)w.X * w.Y * w.Z) / 512;
+    uint32_t top = 0;
+    for (uint64_t b = 0; b < nb; b++) {
+        uint32_t bx, by, bz;
+        brick_coords(w, b, bx, by, bz);
+        const uint32_t t = brick_top_y(&h.brick[bits_word_index(b, 0)], by);
+        top = t > top ? t : top;
+    }
+    return top + 1u < (uint32_t)w.Y ? top + 1u : (uint32_t)w.Y;
+}
+
 template <int G, bool REUSE, bool RW = true>
 Hit trace_v(const World& w, f3 o, f3 d, float t, StepCount& sc) { return trace<true, G, REUSE, RW>(w, o, d, t, sc); }
 }  // namespace
@@ -70,8 +84,28 @@ void rvh_simplex3D(const float* xyz, float* out, int64_t n) {
     for (int64_t i = 0; i < n; i++) out[i] = rv::simplex3D(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
 }
 
+// sky_exit: 1 = World::ytop from the bricks (world_top_y over every brick, as k_world_top), the
+// frame kernels' traversal; 0 = ytop = Y, the reference's step counts.
+static int trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
+                      const float* dir, const float* dist, int64_t n, HostHit* out, int sky_exit);
+
 int rvh_trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
                    const float* dir, const float* dist, int64_t n, HostHit* out) {
+    return trace_rays(variant, lx, ly, lz, bits, csdf, org, dir, dist, n, out, 0);
+}
+
+int rvh_trace_rays_sky_exit(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf,
+                            const float* org, const float* dir, const float* dist, int64_t n, HostHit* out,
+                            uint32_t* ytop) {
+    const int r = trace_rays(variant, lx, ly, lz, bits, csdf, org, dir, dist, n, out, 1);
+    HostWorld h;
+    build(h, lx, ly, lz, bits, csdf);
+    *ytop = world_ytop(h);
+    return r;
+}
+
+static int trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
+                      const float* dir, const float* dist, int64_t n, HostHit* out, int sky_exit) {
     Hit (*fn)(const World&, f3, f3, float, StepCount&) = nullptr;
     switch (variant) {
     case 0: fn = trace_v<1, false>; break;
@@ -85,6 +119,7 @@ int rvh_trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, co
     }
     HostWorld h;
     build(h, lx, ly, lz, bits, csdf);
+    if (sky_exit) h.w.ytop = world_ytop(h);
     for (int64_t i = 0; i < n; i++) {
         StepCount sc{};
         Hit r = fn(h.w, V(org[3 * i], org[3 * i + 1], org[3 * i + 2]),

@@ -144,8 +144,12 @@ def test_c1_full_world_full_frame(rv, atlas, oracle):
         assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"])
         assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"])
         st = r.stats()
-        for k in ("traces", "primary", "sphere_steps", "dda_steps", "csdf_checks", "tex_samples", "undef_hits"):
+        for k in ("traces", "primary", "tex_samples", "undef_hits"):
             assert st[k] == ref["stats"][k], (pose, k)
+        # the frame traversal's sky exit (World::ytop) ends upward rays above the terrain early: the
+        # same hits from fewer steps (the step counts themselves: rv_trace_rays, test_trace_bit_exact)
+        for k in ("sphere_steps", "dda_steps", "csdf_checks"):
+            assert st[k] <= ref["stats"][k], (pose, k)
     r.close()
 
 

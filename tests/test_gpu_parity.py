@@ -144,8 +144,10 @@ def test_frame_parity(rv, atlas, oracle_world, oracle, name, flags, pose):
         assert np.array_equal(hd.view(np.uint32), ref["halfdist"].view(np.uint32))
     os_ = ref["stats"]
     for k in ("traces", "primary", "shadow", "refl", "refl_shadow", "prepass_primary", "prepass_shadow",
-              "cones", "cone_steps", "sphere_steps", "dda_steps", "csdf_checks", "undef_hits"):
+              "cones", "cone_steps", "undef_hits"):
         assert st[k] == os_[k], (k, st[k], os_[k])
+    for k in ("sphere_steps", "dda_steps", "csdf_checks"):   # <=: the sky exit (test_sky_exit_frames_and_gi)
+        assert st[k] <= os_[k], (k, st[k], os_[k])
     r.close()
 
 
@@ -618,3 +620,51 @@ def test_frame_seq_batched_moving_camera(rv, atlas, flags):
             comm.close()
     r.close()
     ref.close()
+
+
+@pytest.mark.parametrize("pose", ["P0", "P1"])
+def test_sky_exit_frames_and_gi(rv, atlas, oracle, pose):
+    """The frame traversal's sky exit (World::ytop = highest solid row + 2,
+    recomputed on every bits write): on a 128^3 world with open sky above
+    y = 90 (rows cleared, CSDF rebuilt, imported through rv_world_import), the
+    reference frame (RGBA8, motion, depth, half-res distance) and a GI update
+    equal the oracle's full march bit for bit, with the same trace and cone
+    counts and fewer sphere steps; rv_trace_rays keeps the reference's step
+    counts exactly."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    lg, W, H = 7, 256, 144
+    flags = rv.RV_FLAGS_REFERENCE
+    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas).build(gi_sweeps=1)
+    vox = ow.voxels()
+    vox[:, 90:, :] = False
+    ow.bits[:] = np.packbits(vox.ravel(), bitorder="little").view(np.uint32)
+    ow.build_csdf()
+    r = rv.StateRender((lg,) * 3, W, H, flags=flags, atlas=atlas)
+    r.world_import(rv.RV_WORLD_BITS, ow.bits)
+    r.world_import(rv.RV_WORLD_CSDF, ow.csdf)
+    r.world_import(rv.RV_WORLD_GI, ow.gi)
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128[pose], W, H)
+    r.stats_reset()
+    r.frame(cam, vp, flags=flags | rv.RV_F_STATS)
+    st = r.stats()
+    ref = oracle.render(ow, oracle.make_frame(W, H, flags, rv.camera_dict(cam, vp)))
+    assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref["rgba"])
+    assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"])
+    assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"])
+    assert np.array_equal(r.readback(rv.RV_IMAGE_HALF_DIST).view(np.uint32), ref["halfdist"].view(np.uint32))
+    os_ = ref["stats"]
+    for k in ("traces", "primary", "refl", "refl_shadow", "prepass_primary", "prepass_shadow", "cones", "cone_steps",
+              "undef_hits"):
+        assert st[k] == os_[k], (k, st[k], os_[k])
+    assert st["sphere_steps"] < os_["sphere_steps"] and st["dda_steps"] <= os_["dda_steps"]
+    # a GI update window: shadow and bounce rays through the same exit
+    r.gi_update(3, first=1000, count=6000)
+    ow.gi_update(3, first=1000, count=6000)
+    assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi)
+    # the trace API: the reference's counts
+    rng = np.random.default_rng(5)
+    org, dirs, dist = random_rays(rng, 4000, (ow.X, ow.Y, ow.Z))
+    g = r.trace_rays(org, dirs, dist)
+    o = ow.trace_batch(org, dirs, dist)
+    assert np.array_equal(g["sphere_steps"], o["n_sphere"]) and np.array_equal(g["dda_steps"], o["n_dda"])
+    r.close()

@@ -90,3 +90,44 @@ def test_simplex3d_equals_oracle(host_lib):
     want = np.empty(len(pts), np.float32)
     O.lib().or_simplex3D_batch(np.ascontiguousarray(pts).ctypes.data, want.ctypes.data, len(pts))
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("variant", ["g1", "g4", "g8", "g4_replay"])
+def test_sky_exit_keeps_every_hit(host_lib, oracle_world, variant):
+    """The frame kernels' sky exit (World::ytop, rv_device.h trace): a ray
+    with dir.y >= 0 that has risen to the highest solid row + 2 stops as a
+    miss.  Every ray's result -- hit, undefined hit, position, normal, uv --
+    equals the oracle's (the reference's full march); only the step counts
+    shrink.  Rays start anywhere, half of them pointing up, on a 128^3 world
+    whose terrain leaves open sky above it."""
+    L = host_lib
+    L.rvh_trace_rays_sky_exit.restype = C.c_int
+    L.rvh_trace_rays_sky_exit.argtypes = [C.c_int] * 4 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p, C.c_void_p]
+    from oracle import oracle as O
+    ow = O.OracleWorld(7, 7, 7).build(gi_sweeps=-1)
+    # open sky above the terrain: clear every voxel row from y = 90 up, then the CSDF again
+    vox = ow.voxels()
+    vox[:, 90:, :] = False
+    ow.bits[:] = np.packbits(vox.ravel(), bitorder="little").view(np.uint32)
+    ow.build_csdf()
+    rng = np.random.default_rng(77)
+    org, d, dist = random_rays(rng, 30000, (ow.X, ow.Y, ow.Z))
+    up = rng.random(len(d)) < 0.5
+    d[up, 1] = np.abs(d[up, 1])
+    d[:200, 1] = 0.0                       # horizontal rays (dir.y == 0: y stays constant)
+    d[200:400, 1] = -0.0
+    g = np.zeros(len(dist), HIT)
+    ytop = C.c_uint32()
+    p = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    assert L.rvh_trace_rays_sky_exit(VARIANTS[variant], ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(org), p(d),
+                                     p(dist), len(dist), p(g), C.byref(ytop)) == 0
+    o = ow.trace_batch(org, d, dist)
+    assert ytop.value == 1 + int(np.flatnonzero(vox.any(axis=(0, 2))).max()) + 1   # highest solid row + 2
+    assert (g["hit"] == o["hit"]).all() and (g["undef"] == o["undef"]).all()
+    assert np.array_equal(g["pos"].view(np.uint32), o["pos"].view(np.uint32))
+    assert np.array_equal(g["normal"], o["normal"])
+    assert np.array_equal(g["u"].view(np.uint32), o["u"].view(np.uint32))
+    assert np.array_equal(g["v"].view(np.uint32), o["v"].view(np.uint32))
+    assert (g["sphere"] <= o["n_sphere"]).all()
+    assert g["sphere"].sum() < 0.9 * o["n_sphere"].sum()   # the exit does cut the march
+    assert g["hit"].mean() > 0.2
