@@ -75,6 +75,7 @@ struct rv_ctx {
     int lx = 0, ly = 0, lz = 0;
     World w{};
     uint32_t* d_top = nullptr;     // world_top scratch (one dword)
+    uint32_t* coltop = nullptr;    // sun horizon: highest solid row + 1 per brick column
     uint32_t* brick = nullptr;
     size_t brick_bytes = 0;
     uint32_t* gi = nullptr;       // current grid
@@ -332,8 +333,9 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     w.SX = w.X / 2; w.SY = w.Y / 2; w.SZ = w.Z / 2;
     w.GX = w.X / 4; w.GY = w.Y / 4; w.GZ = w.Z / 4;
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
-    c->brick_bytes = ((uint64_t)w.X * w.Y * w.Z) / 4;   // 128 B per 512 voxels
     world_set_regions(w, ((uint64_t)w.X * w.Y * w.Z) / 512);
+    // 128 B per 512 voxels (bits and CSDF regions), then the sun horizon (rv_device.h horizon_at)
+    c->brick_bytes = horizon_byte(w.coff) + horizon_bytes(w.X, w.Z);
     c->gi_bytes = n_gi(c) * 4;
 
     auto cleanup_fail = [&](rv_status s, const char* what) {
@@ -344,7 +346,8 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     };
     if (hipMalloc(&c->brick, c->brick_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "bricks");
     if (hipMalloc(&c->gi, c->gi_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "gi");
-    hipMemset(c->brick, 0, c->brick_bytes);
+    hipMemset(c->brick, 0, horizon_byte(w.coff));
+    hipMemset(reinterpret_cast<char*>(c->brick) + horizon_byte(w.coff), 0xFF, horizon_bytes(w.X, w.Z));   // no sun exit
     hipMemset(c->gi, 0, c->gi_bytes);
     // atlas
     int aw = cfg->atlas_rgba8 ? cfg->atlas_w : 256, ah = cfg->atlas_rgba8 ? cfg->atlas_h : 256;
@@ -455,6 +458,7 @@ void rv_destroy(rv_ctx* c) {
     for (FrameSlot& sl : c->slots) slot_free(sl);
     hipFree(c->counters);
     hipFree(c->d_top);
+    hipFree(c->coltop);
     hipFree(c->tiles.d); hipFree(c->untile_ids.d);
     hipFree(c->tilebuf);
     hipFree(c->hpos); hipFree(c->hinfo); hipFree(c->hsec); hipFree(c->pphit); hipFree(c->qcount);
@@ -634,9 +638,13 @@ rv_status rv_sync(rv_ctx* c) {
 }
 
 // The sky exit of the frame traversal (World::ytop, rv_device.h trace): the highest solid voxel
-// row + 2, recomputed after every write of the bits.  Env RV_SKY_EXIT=0 turns it off (ytop = Y).
+// row + 2, and the sun exit of its shadow rays (World::horizon), recomputed after every write of the
+// bits.  Env RV_SKY_EXIT=0 turns both off (ytop = Y, no horizon).
 static rv_status world_top(rv_ctx* c) {
     c->w.ytop = (uint32_t)c->w.Y;
+    uint32_t* hz = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->brick) + horizon_byte(c->w.coff));
+    const size_t hzb = horizon_bytes(c->w.X, c->w.Z);
+    HIP_TRY(c, hipMemsetAsync(hz, 0xFF, hzb, c->stream));   // no sun exit unless built below
     const char* e = getenv("RV_SKY_EXIT");
     if (e && e[0] == '0') return RV_OK;
     if (!c->d_top) HIP_TRY(c, hipMalloc(&c->d_top, 4));
@@ -647,6 +655,19 @@ static rv_status world_top(rv_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(&top, c->d_top, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->w.ytop = std::min((uint32_t)c->w.Y, top + 1u);   // top = max solid y + 1
+    // the sun exit of shadow rays (trace_sun): the horizon per brick column for the library's sun
+    // (env RV_SUN_EXIT=0: off)
+    const char* se = getenv("RV_SUN_EXIT");
+    const f3 sun = sun_dir();
+    const double hxz = std::sqrt((double)sun.x * sun.x + (double)sun.z * sun.z);
+    if ((se && se[0] == '0') || !(sun.y > 0.0f) || hxz == 0.0) return RV_OK;
+    if (!c->coltop) HIP_TRY(c, hipMalloc(&c->coltop, hzb));
+    HIP_TRY(c, hipMemsetAsync(c->coltop, 0, hzb, c->stream));
+    // slope shaded 0.1 % low (a lower slope only raises the horizon: conservative)
+    const float k = (float)((double)sun.y / hxz * (1.0 - 1e-3));
+    launch_sun_horizon(c->stream, c->brick, current_world(c), c->coltop, hz, (float)(sun.x / hxz),
+                       (float)(sun.z / hxz), k);
+    LAUNCH_CHECK(c);
     return RV_OK;
 }
 
@@ -1284,7 +1305,8 @@ rv_status rv_trace_rays(rv_ctx* c, const float* org, const float* dir, const flo
     HIP_TRY(c, hipMemcpyAsync(d_d, dir, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(d_t, dist, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
     World tw = current_world(c);
-    tw.ytop = (uint32_t)tw.Y;   // rv_trace_rays reports the reference's step counts: no sky exit
+    tw.ytop = (uint32_t)tw.Y;   // rv_trace_rays reports the reference's step counts: no sky exit (and it
+                                // traces no sun rays through trace_sun)
     launch_trace_rays(c->stream, tw, d_o, d_d, d_t, n, d_h);
     LAUNCH_CHECK(c);
     HIP_TRY(c, hipMemcpyAsync(out, d_h, (size_t)n * sizeof(RvHitDev), hipMemcpyDeviceToHost, c->stream));

@@ -37,7 +37,7 @@ namespace rv {
 // RV_ABLATE (timing experiments only, never the product): bits that skip a
 // part of the frame to price it -- 1 texture noise, 2 cones, 4 water
 // reflection, 8 fog, 16 MV/depth stores, 32/64/128 the GI / pre-pass / render
-// part of the pipelined launch, 256/512 the GI update's shadow / bounce ray.
+// part of the pipelined launch, 256/512 the GI update's shadow / bounce ray, 1024 the pre-pass shadow ray.
 #ifndef RV_ABLATE
 #define RV_ABLATE 0
 #endif
@@ -180,6 +180,12 @@ RV_HD void world_set_brick(World& w, const uint32_t* brick) {
     w.brick = brick;
     w.csdf = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(brick) + w.coff);
 }
+
+// The sun horizon (trace_sun's exit, horizon_column): one dword per brick column, index bx | bz << lbx,
+// stored right after the CSDF region in the same allocation (no extra kernel argument: its base is
+// the brick base + 2 coff).  UINT32_MAX everywhere = no sun exit.
+__host__ __device__ inline size_t horizon_byte(uint32_t coff) { return 2 * (size_t)coff; }
+__host__ __device__ inline size_t horizon_bytes(int X, int Z) { return (size_t)(X >> 3) * (size_t)(Z >> 3) * 4; }
 
 // Brick storage.  RV_SPLIT_BRICKS=0: one 128-B record per 8^3 brick, 64 B of
 // bits then 64 B of CSDF (coff = 64).  RV_SPLIT_BRICKS=1: a bits region of
@@ -328,6 +334,11 @@ RV_HD uint32_t voxel_bit(const LinearWorld&, uint32_t x, uint32_t) { return x & 
 RV_HD uint32_t voxel_shift(const LinearWorld&, uint32_t x, uint32_t) { return x & 31u; }
 RV_HD uint32_t gi_texel(const LinearWorld& w, uint32_t idx) { return w.gi[idx]; }
 // GI grid (X/4 x Y/4 x Z/4, x fastest, power-of-two dims < 2^32 cells): log2 GX, log2 (GX * GY)
+RV_HD uint32_t horizon_at(const World& w, uint32_t x, uint32_t z) {
+    const uint32_t* hz = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + horizon_byte(w.coff));
+    return hz[(x >> 3) | ((z >> 3) << w.lbx)];
+}
+RV_HD uint32_t horizon_at(const LinearWorld&, uint32_t, uint32_t) { return 0xFFFFFFFFu; }   // no sun exit
 RV_HD uint32_t gi_shift_x(const World& w) { return (uint32_t)w.lbx + 1u; }
 RV_HD uint32_t gi_shift_xy(const World& w) { return (uint32_t)w.lbxy + 2u; }
 RV_HD uint32_t gi_shift_x(const LinearWorld& w) { return (uint32_t)w.lx - 2u; }
@@ -684,8 +695,10 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 // RW: look-ahead groups by stop search + re-walk (default) or by the step-by-step replay with an
 // early exit (round 1-2; kept for A/B and checked bit-exact on the CPU, tests/test_host_trace.py).
 // Re-walk: C4 0.667 -> 0.631 ms, C3 0.282 -> 0.270 (profiles/r02/rewalk_ab.txt).
+// SUN (trace_sun): the ray's direction is the sun's, and World::horizon (when set) holds, per brick
+// column, a height from which a ray toward the sun can no longer meet a solid voxel (the sun exit).
 template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0), bool RW = (RV_DDA_REWALK != 0),
-          class WV = World>
+          bool SUN = false, class WV = World>
 RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     Hit H;
     H.hit = false; H.undef = false; H.its = 0;
@@ -716,6 +729,8 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         for (int it = 0; it < 100; it++) {
             const int fx = floor_i(cur.x), fy = floor_i(cur.y), fz = floor_i(cur.z);
             oob = ((uint32_t)fx >= X) | ((uint32_t)fy >= YL) | ((uint32_t)fz >= Z);
+            if (SUN)   // the gather overlaps the step's CSDF gather
+                oob = oob | ((uint32_t)fy >= horizon_at(w, umin((uint32_t)fx, X - 1u), umin((uint32_t)fz, Z - 1u)));
             uint32_t d;
             if (REUSE) {   // gather only where the CSDF dword changed
                 const uint32_t cx = umin((uint32_t)(fx >> 1), (uint32_t)w.SX - 1u);
@@ -997,6 +1012,52 @@ RV_HD Hit trace(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
         }
     }
     return H;
+}
+
+// A ray toward the sun (shadow rays: its direction is exactly the sun vector the horizon was built for).
+#ifndef RV_SUN_HORIZON   // 0: shadow rays without the sun exit (A/B builds)
+#define RV_SUN_HORIZON 1
+#endif
+template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0), class WV = World>
+RV_HD Hit trace_sun(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
+    return trace<COUNT, G, REUSE, (RV_DDA_REWALK != 0), (RV_SUN_HORIZON != 0), WV>(w, cam, dir, dist_h, sc);
+}
+
+// Sun horizon of brick column (bx, bz) (World::horizon, the sun exit).  A ray toward the sun (slope
+// k = rise per unit of horizontal travel > 0, horizontal direction (ux, uz)) that starts in this column
+// at a height y passes over column c' only after a horizontal travel h >= hmin(c'), at a height
+// >= y + k h; it can meet a solid voxel of c' only if that height is below top(c') + 2 (the margin of
+// the sky exit).  The column's samples q(t) = its centre + t (ux, uz), t = 0, 8, 16, ... cover the band
+// that rays from any point of the column sweep (a point of the ray is within 5.7 + 4 voxels of a
+// sample; the 5 x 5 brick columns around a sample reach >= 16 voxels out), and every column of a
+// sample's neighbourhood is >= t - 34 away horizontally.  Returns max over samples of
+// (top + 2 - k max(0, t - 34)), rounded up: at or above it the ray can only miss.  coltop = highest
+// solid row + 1 per brick column (0: empty).
+RV_HD uint32_t horizon_column(const uint32_t* coltop, int nbx, int nbz, int lbx, int bx, int bz, float ux, float uz,
+                              float k) {
+    float H = 0.0f;
+    const float cx = (float)bx * 8.0f + 4.0f, cz = (float)bz * 8.0f + 4.0f;
+    const float ext = 8.0f * (float)(nbx > nbz ? nbx : nbz) + 48.0f;
+    for (int i = 0;; i++) {
+        const float t = 8.0f * (float)i;
+        const float qx = cx + t * ux, qz = cz + t * uz;
+        if (qx < -48.0f || qz < -48.0f || qx > 8.0f * (float)nbx + 48.0f || qz > 8.0f * (float)nbz + 48.0f || t > 2.0f * ext)
+            break;
+        const int sx = (int)floorf(qx * 0.125f), sz = (int)floorf(qz * 0.125f);
+        uint32_t m = 0;
+        for (int dz = -2; dz <= 2; dz++)
+            for (int dx = -2; dx <= 2; dx++) {
+                const int x = sx + dx, z = sz + dz;
+                if (x < 0 || z < 0 || x >= nbx || z >= nbz) continue;
+                const uint32_t v = coltop[(uint32_t)x | ((uint32_t)z << lbx)];
+                m = v > m ? v : m;
+            }
+        if (m) {
+            const float h = (float)m + 2.0f - k * (t > 34.0f ? t - 34.0f : 0.0f);
+            H = h > H ? h : H;
+        }
+    }
+    return (uint32_t)ceilf(H);
 }
 
 // tanf(0.4f), correctly rounded (see oracle OR_TAN_CONE).

@@ -53,9 +53,9 @@ __device__ __forceinline__ void prepass_pixel(const WV& w, const FrameParams& f,
     float d = h.hit ? length(sub(h.pos, f.pos)) : 300.0f;
     float s = 1.0f;
     if (STATS) { c[CNT_TRACES]++; c[CNT_PP_PRIMARY]++; c[CNT_UNDEF] += h.undef; }
-    if (h.hit) {
+    if (h.hit && !(RV_ABLATE & 1024)) {
         RV_GD_KIND(gd::PP_SHADOW);
-        Hit sh = trace<STATS, RV_G_PREPASS, false>(w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
+        Hit sh = trace_sun<STATS, RV_G_PREPASS, false>(w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
         s = sh.hit ? SHADOW_HIT : 1.0f;
         if (STATS) { c[CNT_TRACES]++; c[CNT_PP_SHADOW]++; }
     }
@@ -155,7 +155,7 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         if (rh.hit) {
             rc = sample_texture(w, rh.u, rh.v, rh.pos);
             RV_GD_KIND(gd::REFL_SHADOW);
-            Hit rs = trace<STATS, G, RE>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
+            Hit rs = trace_sun<STATS, G, RE>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
             if (STATS) { c[CNT_TRACES]++; c[CNT_REFL_SHADOW]++; c[CNT_TEX]++; }
             if (rs.hit) rc = scale(rc, 0.1f);
         } else {
@@ -172,7 +172,7 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
             shadow = 1.0f;
             if (has<FEAT>(f, RV_F_SHADOW)) {
                 RV_GD_KIND(gd::SHADOW);
-                Hit sh = trace<STATS, G, RE>(w, add(hit.pos, scale(hit.normal, 1e-1f)), f.sun, 0.0f, sc);
+                Hit sh = trace_sun<STATS, G, RE>(w, add(hit.pos, scale(hit.normal, 1e-1f)), f.sun, 0.0f, sc);
                 if (STATS) { c[CNT_TRACES]++; c[CNT_SHADOW]++; }
                 shadow = sh.hit ? SHADOW_HIT : 1.0f;
             }

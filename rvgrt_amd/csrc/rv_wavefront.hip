@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(256) k_wf_pp_shadow(World w, FrameParams f) {
         float4 hp = f.pphit[p];
         f3 pos = V(hp.x, hp.y, hp.z), nrm = normal_of(__float_as_uint(hp.w));
         StepCount sc{};
-        Hit sh = trace<STATS>(w, add(pos, scale(nrm, 1e-1f)), f.sun, 0.0f, sc);
+        Hit sh = trace_sun<STATS>(w, add(pos, scale(nrm, 1e-1f)), f.sun, 0.0f, sc);
         f.hshadow[p] = sh.hit ? SHADOW_HIT : 1.0f;
         if (STATS) {
             c[CNT_TRACES]++; c[CNT_PP_SHADOW]++;
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256) k_wf_shadow(World w, FrameParams f) {
         uint32_t info = f.hinfo[p];
         f3 pos = V(hp.x, hp.y, hp.z), nrm = normal_of(info >> HI_NSHIFT);
         StepCount sc{};
-        Hit sh = trace<STATS>(w, add(pos, scale(nrm, 1e-1f)), f.sun, 0.0f, sc);
+        Hit sh = trace_sun<STATS>(w, add(pos, scale(nrm, 1e-1f)), f.sun, 0.0f, sc);
         if (sh.hit) f.hinfo[p] = info | HI_SHADOWED;
         if (STATS) {
             c[CNT_TRACES]++; c[CNT_SHADOW]++;
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(256) k_wf_water(World w, FrameParams f) {
         f3 rc;
         if (rh.hit) {
             rc = sample_texture(w, rh.u, rh.v, rh.pos);
-            Hit rs = trace<STATS>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
+            Hit rs = trace_sun<STATS>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
             if (rs.hit) rc = scale(rc, 0.1f);
         } else {
             rc = sample_sky(rdir, f.sun);

@@ -5,6 +5,8 @@
 // hosts without a GPU.  Not linked into librvgrt_hip.so and not used by it.
 #include <stdint.h>
 #include <string.h>
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "../../rvgrt_amd/csrc/rv_device.h"
@@ -29,7 +31,9 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
     const uint64_t nbricks = ((uint64_t)w.X * w.Y * w.Z) / 512;
     world_set_regions(w, nbricks);
-    h.brick.assign((size_t)(((uint64_t)w.X * w.Y * w.Z) / 16), 0u);   // 128 B per brick
+    // 128 B per brick, then the sun horizon (UINT32_MAX: no sun exit until world_horizon builds it)
+    h.brick.assign((size_t)(((uint64_t)w.X * w.Y * w.Z) / 16) + horizon_bytes(w.X, w.Z) / 4, 0u);
+    std::fill(h.brick.begin() + (long)(horizon_byte(w.coff) / 4), h.brick.end(), 0xFFFFFFFFu);
     for (uint64_t z = 0; z < (uint64_t)w.Z; z++)
         for (uint64_t y = 0; y < (uint64_t)w.Y; y++)
             for (uint64_t x = 0; x < (uint64_t)w.X; x++) {
@@ -61,6 +65,30 @@ uint32_t world_ytop(const HostWorld& h) {
         top = t > top ? t : top;
     }
     return top + 1u < (uint32_t)w.Y ? top + 1u : (uint32_t)w.Y;
+}
+
+// World::horizon as rv_abi.cpp's world_top builds it for the sun direction `sun` (k_column_top +
+// k_horizon: the same horizon_column)
+void world_horizon(HostWorld& h, const float* sun, std::vector<uint32_t>& coltop, std::vector<uint32_t>& hz) {
+    World& w = h.w;
+    const int nbx = w.X >> 3, nbz = w.Z >> 3;
+    coltop.assign((size_t)nbx * nbz, 0u);
+    hz.assign((size_t)nbx * nbz, 0u);
+    const uint64_t nb = ((uint64_t)w.X * w.Y * w.Z) / 512;
+    for (uint64_t b = 0; b < nb; b++) {
+        uint32_t bx, by, bz;
+        brick_coords(w, b, bx, by, bz);
+        const uint32_t t = brick_top_y(&h.brick[bits_word_index(b, 0)], by);
+        uint32_t& c = coltop[bx | (bz << (uint32_t)w.lbx)];
+        c = t > c ? t : c;
+    }
+    const double hxz = std::sqrt((double)sun[0] * sun[0] + (double)sun[2] * sun[2]);
+    const float k = (float)((double)sun[1] / hxz * (1.0 - 1e-3));
+    for (int bz = 0; bz < nbz; bz++)
+        for (int bx = 0; bx < nbx; bx++)
+            hz[(uint32_t)bx | ((uint32_t)bz << w.lbx)] = horizon_column(coltop.data(), nbx, nbz, w.lbx, bx, bz,
+                                                                        (float)(sun[0] / hxz), (float)(sun[2] / hxz), k);
+    std::copy(hz.begin(), hz.end(), h.brick.begin() + (long)(horizon_byte(w.coff) / 4));   // where horizon_at reads
 }
 
 template <int G, bool REUSE, bool RW = true>
@@ -102,6 +130,31 @@ int rvh_trace_rays_sky_exit(int variant, int lx, int ly, int lz, const uint32_t*
     build(h, lx, ly, lz, bits, csdf);
     *ytop = world_ytop(h);
     return r;
+}
+
+// Rays toward the sun through trace_sun with the sky exit and the sun horizon built for `sun`
+// (every direction must be exactly `sun`, as for the kernels' shadow rays); hz_out: the horizon map.
+int rvh_trace_sun(int g8, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* sun,
+                  const float* org, const float* dist, int64_t n, HostHit* out, uint32_t* hz_out) {
+    HostWorld h;
+    build(h, lx, ly, lz, bits, csdf);
+    h.w.ytop = world_ytop(h);
+    std::vector<uint32_t> coltop, hz;
+    world_horizon(h, sun, coltop, hz);
+    memcpy(hz_out, hz.data(), hz.size() * 4);
+    const f3 d = V(sun[0], sun[1], sun[2]);
+    for (int64_t i = 0; i < n; i++) {
+        StepCount sc{};
+        const f3 o = V(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
+        Hit r = g8 ? trace_sun<true, 8, false>(h.w, o, d, hround(dist[i]), sc)
+                   : trace_sun<true, 4, false>(h.w, o, d, hround(dist[i]), sc);
+        HostHit& q = out[i];
+        q.pos[0] = r.pos.x; q.pos[1] = r.pos.y; q.pos[2] = r.pos.z;
+        q.normal[0] = r.normal.x; q.normal[1] = r.normal.y; q.normal[2] = r.normal.z;
+        q.u = r.u; q.v = r.v; q.hit = r.hit; q.undef = r.undef;
+        q.sphere = (int)sc.sphere; q.dda = (int)sc.dda; q.check = (int)sc.check; q.pad = 0;
+    }
+    return 0;
 }
 
 static int trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,

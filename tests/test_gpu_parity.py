@@ -285,8 +285,8 @@ def test_golden_frames(rv, atlas):
         assert sha(r.readback(rv.RV_IMAGE_MOTION)) == fr["mv"], key
         assert sha(r.readback(rv.RV_IMAGE_DEPTH)) == fr["depth"], key
         st = r.stats()
-        for k, v in fr["stats"].items():
-            assert st[k] == v, (key, k, st[k], v)
+        for k, v in fr["stats"].items():   # the step counts of the full march, or fewer (the sky / sun exits)
+            assert (st[k] <= v) if k in ("sphere_steps", "dda_steps", "csdf_checks") else (st[k] == v), (key, k, st[k], v)
         with open(os.path.join(gdir, f"{key}.png"), "rb") as f:
             want = decode_png(f.read())
         d = np.abs(img.astype(np.int32) - want.astype(np.int32)).max(axis=2)

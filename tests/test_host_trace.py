@@ -131,3 +131,51 @@ def test_sky_exit_keeps_every_hit(host_lib, oracle_world, variant):
     assert (g["sphere"] <= o["n_sphere"]).all()
     assert g["sphere"].sum() < 0.9 * o["n_sphere"].sum()   # the exit does cut the march
     assert g["hit"].mean() > 0.2
+
+
+@pytest.mark.parametrize("g8", [0, 1])
+@pytest.mark.parametrize("sky", ["cut", "full"])
+def test_sun_exit_keeps_every_shadow_hit(host_lib, oracle_world, g8, sky):
+    """The shadow rays' sun exit (trace_sun with World::horizon, built per brick
+    column from the column tops for the sun direction, rv_device.h
+    horizon_column): a ray toward the sun stops as a miss once it is above its
+    column's horizon.  Shadow rays from the voxel surfaces (as the pre-pass,
+    the reflection shadow and the GI update cast them) and from anywhere in the
+    world give the oracle's hit / miss, position, normal and uv exactly, with
+    fewer sphere steps -- on the full 128^3 terrain (no sky above it) and with
+    open sky above row 90."""
+    from oracle import oracle as O
+    L = host_lib
+    L.rvh_trace_sun.restype = C.c_int
+    L.rvh_trace_sun.argtypes = [C.c_int] * 4 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p, C.c_void_p]
+    ow = O.OracleWorld(7, 7, 7).build(gi_sweeps=-1)
+    if sky == "cut":
+        vox = ow.voxels()
+        vox[:, 90:, :] = False
+        ow.bits[:] = np.packbits(vox.ravel(), bitorder="little").view(np.uint32)
+        ow.build_csdf()
+    sun = np.ascontiguousarray(O.sun_dir(), np.float32)
+    rng = np.random.default_rng(9)
+    # surface points: primary hits of random rays, offset along the normal as the kernels do
+    org0, d0, dist0 = random_rays(rng, 40000, (ow.X, ow.Y, ow.Z))
+    h0 = ow.trace_batch(org0, d0, dist0)
+    sel = (h0["hit"] != 0) & (h0["undef"] == 0)
+    surf = (h0["pos"][sel] + h0["normal"][sel] * np.float32(0.1)).astype(np.float32)
+    org = np.ascontiguousarray(np.concatenate([surf, org0[:10000]]), np.float32)
+    dist = np.zeros(len(org), np.float32)
+    dirs = np.ascontiguousarray(np.broadcast_to(sun, org.shape), np.float32)
+    g = np.zeros(len(org), HIT)
+    hz = np.zeros((ow.Z // 8) * (ow.X // 8), np.uint32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    assert L.rvh_trace_sun(g8, ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(sun), p(org), p(dist), len(org), p(g),
+                           p(hz)) == 0
+    o = ow.trace_batch(org, dirs, dist)
+    assert (g["hit"] == o["hit"]).all() and (g["undef"] == o["undef"]).all()
+    assert np.array_equal(g["pos"].view(np.uint32), o["pos"].view(np.uint32))
+    assert np.array_equal(g["normal"], o["normal"])
+    assert np.array_equal(g["u"].view(np.uint32), o["u"].view(np.uint32))
+    assert np.array_equal(g["v"].view(np.uint32), o["v"].view(np.uint32))
+    assert (g["sphere"] <= o["n_sphere"]).all()
+    assert 0.1 < o["hit"].mean() < 0.9                      # shadowed and lit points both
+    assert g["sphere"].sum() < 0.8 * o["n_sphere"].sum()    # the horizon does cut the march
+    assert hz.min() < hz.max()                               # the horizon varies over the terrain
