@@ -376,7 +376,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
-    if (const char* e = getenv("RV_GROUP")) c->group = std::min(16, std::max(0, atoi(e)));
+    if (const char* e = getenv("RV_GROUP")) c->group = std::min(32, std::max(0, atoi(e)));
     if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
         if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
         c->gather_bpp = atoi(e);
@@ -615,7 +615,7 @@ rv_status rv_set_pipeline(rv_ctx* c, int32_t on) {
 }
 
 rv_status rv_set_frame_group(rv_ctx* c, int32_t n) {
-    if (!c || n < 0 || n > 16) return RV_ERR_INVALID;
+    if (!c || n < 0 || n > 32) return RV_ERR_INVALID;
     c->group = n;
     c->carry_gi = c->carry_pp = false;
     return RV_OK;
@@ -2072,7 +2072,7 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
 // records of a group all-gathered once; the packed tiles of group g go to rank 0 after launch g.
 static int group_frames(const rv_ctx* c) {
     const uint64_t n = n_gi(c), rays = std::min<uint64_t>(c->cfg.gi_rays_per_frame, n);
-    int F = std::min(c->group, 16);
+    int F = std::min(c->group, 32);
     while (F >= 2 && (uint64_t)F * rays * 2 > n) F--;   // two groups' updates never overlap in the grid
     return F >= 2 ? F : 0;
 }

@@ -33,7 +33,7 @@ def _ref_step(rv, ref, d, flags):
 
 
 @pytest.mark.parametrize("F,rays,order", [(2, 5000, "102"), (3, 5000, "012"), (4, 2048, "102"), (8, 2048, "210"),
-                                          (8, 1000, "102")])
+                                          (8, 1000, "102"), (32, 500, "102")])
 def test_grouped_frames_equal_one_at_a_time(rv, atlas, oracle, monkeypatch, F, rays, order):
     """128^3 world (32768 GI cells): windows of 5000 (partial last window,
     linear cell order), 2048 (whole planes, blocked order) and 1000 cells;
