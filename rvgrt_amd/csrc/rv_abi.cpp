@@ -82,6 +82,7 @@ struct rv_ctx {
     uint32_t* gi_tmp = nullptr;   // update target (double buffer)
     size_t gi_bytes = 0;
     uint32_t* atlas = nullptr;
+    uint32_t* tex = nullptr;      // sampleTexture's tile table (World::tex), or null
     // frame images (library-owned unless bound)
     uint32_t* color = nullptr; size_t color_pitch = 0; bool color_ext = false;
     uint32_t* mv = nullptr; size_t mv_pitch = 0; bool mv_ext = false;
@@ -361,6 +362,22 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
         hipMemcpy(c->atlas, grey.data(), grey.size() * 4, hipMemcpyHostToDevice);
     }
     c->cfg.atlas_rgba8 = nullptr;
+    // sampleTexture's tile table (World::tex, rv_device.h tex_index): 4 B per voxel, a function of the
+    // voxel coordinates only, so it is built once here.  Env RV_TEX_TABLE=0, or no memory for it,
+    // leaves the noise evaluation in the kernels (identical tiles).
+    const char* te = getenv("RV_TEX_TABLE");
+    if (!(te && te[0] == '0')) {
+        const size_t tb = (size_t)w.X * w.Y * w.Z * 4;
+        if (hipMalloc(&c->tex, tb) == hipSuccess) {
+            launch_tex_table(c->stream, c->tex, w);
+            if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+                return cleanup_fail(RV_ERR_HIP, "tex table");
+            w.tex = c->tex;
+        } else {
+            c->tex = nullptr;
+            (void)hipGetLastError();
+        }
+    }
     // frame slot 0 (more with rv_set_frames_in_flight)
     int W = cfg->width, H = cfg->height;
     c->own_color_pitch = align256((size_t)W * 4);
@@ -425,7 +442,7 @@ void rv_destroy(rv_ctx* c) {
     } else {
         hipDeviceSynchronize();   // every frame slot's stream
     }
-    hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas);
+    hipFree(c->brick); hipFree(c->gi); hipFree(c->gi_tmp); hipFree(c->atlas); hipFree(c->tex);
     for (auto& ph : c->pipe_half) { hipFree(ph[0]); hipFree(ph[1]); }
     for (int q = 0; q < 2; q++) { hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]); }
     hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);

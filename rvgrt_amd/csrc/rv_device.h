@@ -174,6 +174,8 @@ struct World {
     uint32_t ytop;                       // sky exit (trace): max solid y + 2, or Y (no exit)
     const uint32_t* __restrict__ csdf;   // = brick + coff: the CSDF region's own base, so a CSDF
                                          // gather is SGPR base + the brick-relative offset
+    const uint32_t* __restrict__ tex;    // sampleTexture's atlas tile per voxel (tex_entry), or null:
+                                         // evaluated from the noise in the kernel
 };
 // Point a world view at its brick records (both region bases).
 RV_HD void world_set_brick(World& w, const uint32_t* brick) {
@@ -339,6 +341,26 @@ RV_HD uint32_t horizon_at(const World& w, uint32_t x, uint32_t z) {
     return hz[(x >> 3) | ((z >> 3) << w.lbx)];
 }
 RV_HD uint32_t horizon_at(const LinearWorld&, uint32_t, uint32_t) { return 0xFFFFFFFFu; }   // no sun exit
+
+// sampleTexture's tile table (World::tex, built by k_tex_table at rv_create).  The atlas tile the
+// reference picks (src/raytracing_functions.cu:41-54) is a function of integer lattice points only:
+// eval1 at (floor x, floor y, floor z) and eval2 at (floor(x + 121.3), floor(y + 1321.3),
+// floor(z + 721.5)) = floor(p) + (121, 1321, 721) + a carry of 0 or 1 per axis.  One dword per voxel
+// holds the tile of all 8 carry combinations, 4 bits each (bx | by << 2, bx 0..3, by 0..2), at
+// nibble cx | cy << 1 | cz << 2.  Bricks of 8^3 entries in the world's brick order, (z, x, y)
+// fastest to slowest inside a brick, so a wave's hits on one terrain level read one or two lines.
+RV_HD uint64_t tex_index(const World& w, uint32_t x, uint32_t y, uint32_t z) {
+    const uint64_t b = (uint64_t)(z >> 3) | ((uint64_t)(y >> 3) << w.lbz) | ((uint64_t)(x >> 3) << w.lbzy);
+    return (b << 9) | (z & 7u) | ((x & 7u) << 3) | ((y & 7u) << 6);
+}
+// The entry of lattice point (ix, iy, iz) when the table covers it (false: evaluate the noise).
+RV_HD bool tex_entry(const World& w, int ix, int iy, int iz, uint32_t& e) {
+    if (!w.tex || (uint32_t)ix >= (uint32_t)w.X || (uint32_t)iy >= (uint32_t)w.Y || (uint32_t)iz >= (uint32_t)w.Z)
+        return false;
+    e = w.tex[tex_index(w, (uint32_t)ix, (uint32_t)iy, (uint32_t)iz)];
+    return true;
+}
+RV_HD bool tex_entry(const LinearWorld&, int, int, int, uint32_t&) { return false; }
 RV_HD uint32_t gi_shift_x(const World& w) { return (uint32_t)w.lbx + 1u; }
 RV_HD uint32_t gi_shift_xy(const World& w) { return (uint32_t)w.lbxy + 2u; }
 RV_HD uint32_t gi_shift_x(const LinearWorld& w) { return (uint32_t)w.lx - 2u; }
@@ -1221,24 +1243,25 @@ RV_HD f3 sample_sky(f3 dir, f3 sun) {
 // point filter + wrap on a 256x256 RGBA8 atlas, texel = byte/255.
 template <class WV>
 RV_HD uint32_t sample_texel(const WV& w, float u, float v, f3 pos);
+// the atlas texel of tile 0xYX at fp16 UV (u, v): :56-59
+template <class WV>
+RV_HD uint32_t sample_tile(const WV& w, float u, float v, int tile);
 RV_HD f3 texel_rgb(uint32_t t) { return V(u8f(t & 255u), u8f((t >> 8) & 255u), u8f((t >> 16) & 255u)); }
 template <class WV>
 RV_HD f3 sample_texture(const WV& w, float u, float v, f3 pos) {
     return texel_rgb(sample_texel(w, u, v, pos));
 }
 // the atlas texel sampleTexture reads (its colour is texel_rgb of it)
-template <class WV>
-RV_HD uint32_t sample_texel(const WV& w, float u, float v, f3 pos) {
+// sampleTexture's noise value at lattice point f (eval) and g (eval2), src/raytracing_functions.cu:41-44
+RV_HD float tex_noise(float fx, float fy, float fz, float gx, float gy, float gz) {
     const float freq = 0.05f;
-    float e = 0.5f;
-    if (!(RV_ABLATE & 1)) {
-    e = simplex3D(floorf(pos.x) * freq, floorf(pos.y) * freq, floorf(pos.z) * freq);
-    float e2 = simplex3D(floorf((float)((double)pos.x + 121.3)) * freq * 0.3f,
-                         floorf((float)((double)pos.y + 1321.3)) * freq * 0.3f,
-                         floorf((float)((double)pos.z + 721.5)) * freq * 0.3f);
-    e = e * 0.4f + e2 * 0.6f;
-    }
-    // (bx,by) in 1/16 units: the first threshold e is below, as a select chain (no branches)
+    const float e = simplex3D(fx * freq, fy * freq, fz * freq);
+    const float e2 = simplex3D(gx * freq * 0.3f, gy * freq * 0.3f, gz * freq * 0.3f);
+    return e * 0.4f + e2 * 0.6f;
+}
+// The atlas tile of noise value e (:46-54) as 0xYX in 1/16 units: the first threshold e is below,
+// as a select chain (no branches)
+RV_HD int tex_tile(float e) {
     int tile = 0x10;                   // stone
     tile = e < 1.2f ? 0x00 : tile;     // stone2  (0,0)
     tile = e < 0.8f ? 0x20 : tile;     // dirt    (0,2)
@@ -1248,6 +1271,43 @@ RV_HD uint32_t sample_texel(const WV& w, float u, float v, f3 pos) {
     tile = e < -0.7f ? 0x12 : tile;    // iron    (2,1)
     tile = e < -1.2f ? 0x23 : tile;    // diamond (3,2)
     tile = e < -1.3f ? 0x10 : tile;    // stone   (0,1)
+    return tile;
+}
+// One World::tex entry: the tiles of lattice point (x, y, z) for the 8 carries (tex_index)
+RV_HD uint32_t tex_table_entry(uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t e = 0;
+    for (uint32_t c = 0; c < 8; c++) {
+        const int t = tex_tile(tex_noise((float)x, (float)y, (float)z, (float)(x + 121u + (c & 1u)),
+                                         (float)(y + 1321u + ((c >> 1) & 1u)), (float)(z + 721u + (c >> 2))));
+        e |= (uint32_t)((t & 15) | ((t >> 4) << 2)) << (4 * c);
+    }
+    return e;
+}
+// The atlas tile sampleTexture picks for a hit at pos (0xYX): World::tex's entry when the table
+// covers floor(pos) and the carries g - floor(pos) - offset are 0/1 (always, for a position inside
+// the world), else the noise itself
+template <class WV>
+RV_HD int texture_tile(const WV& w, f3 pos) {
+    if (RV_ABLATE & 1) return tex_tile(0.5f);
+    const float fx = floorf(pos.x), fy = floorf(pos.y), fz = floorf(pos.z);
+    const float gx = floorf((float)((double)pos.x + 121.3)), gy = floorf((float)((double)pos.y + 1321.3)),
+                gz = floorf((float)((double)pos.z + 721.5));
+    const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
+    const uint32_t cx = (uint32_t)(int)gx - (uint32_t)ix - 121u, cy = (uint32_t)(int)gy - (uint32_t)iy - 1321u,
+                   cz = (uint32_t)(int)gz - (uint32_t)iz - 721u;
+    uint32_t ent;
+    if ((cx | cy | cz) <= 1u && tex_entry(w, ix, iy, iz, ent)) {
+        const uint32_t t = (ent >> (4u * (cx | (cy << 1) | (cz << 2)))) & 15u;
+        return (int)((t & 3u) | ((t >> 2) << 4));
+    }
+    return tex_tile(tex_noise(fx, fy, fz, gx, gy, gz));
+}
+template <class WV>
+RV_HD uint32_t sample_texel(const WV& w, float u, float v, f3 pos) {
+    return sample_tile(w, u, v, texture_tile(w, pos));
+}
+template <class WV>
+RV_HD uint32_t sample_tile(const WV& w, float u, float v, int tile) {
     float bx = (float)(tile & 15) * (1.0f / 16.0f), by = (float)(tile >> 4) * (1.0f / 16.0f);
     float ux = hround(hround(u * 0.0625f) + bx);
     float uy = hround(hround(v * 0.0625f) + by);

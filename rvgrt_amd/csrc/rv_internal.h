@@ -160,6 +160,8 @@ uint32_t wf_producer_blocks(const FrameParams& f, int q, bool tiles);
 // column tops (pre-zeroed) and the sun horizon of every brick column (World::horizon; slope k, direction (ux, uz))
 void launch_sun_horizon(hipStream_t s, const uint32_t* brick, const World& w, uint32_t* coltop, uint32_t* horizon,
                         float ux, float uz, float k);
+// sampleTexture's tile table of every voxel (World::tex, 4 B per voxel)
+void launch_tex_table(hipStream_t s, uint32_t* tex, const World& w);
 // the world's highest solid row + 1 into *top (device, pre-zeroed): World::ytop = it + 1
 void launch_world_top(hipStream_t s, const uint32_t* brick, const World& w, uint32_t* top);
 void launch_prepass(hipStream_t s, const World& w, const FrameParams& f);

@@ -112,6 +112,25 @@ void rvh_simplex3D(const float* xyz, float* out, int64_t n) {
     for (int64_t i = 0; i < n; i++) out[i] = rv::simplex3D(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
 }
 
+// sampleTexture's tile (0xYX) for n positions in a 2^lx x 2^ly x 2^lz world, through the World::tex
+// table (built on the host with k_tex_table's element function) and through the noise (tex = null)
+void rvh_texture_tiles(int lx, int ly, int lz, const float* pos, int64_t n, int32_t* via_table, int32_t* via_noise) {
+    World w{};
+    w.X = 1 << lx; w.Y = 1 << ly; w.Z = 1 << lz;
+    w.lbz = lz - 3; w.lbzy = (lz - 3) + (ly - 3);
+    std::vector<uint32_t> tex((size_t)w.X * w.Y * w.Z);
+    for (uint32_t z = 0; z < (uint32_t)w.Z; z++)
+        for (uint32_t y = 0; y < (uint32_t)w.Y; y++)
+            for (uint32_t x = 0; x < (uint32_t)w.X; x++) tex[tex_index(w, x, y, z)] = tex_table_entry(x, y, z);
+    World wn = w;
+    w.tex = tex.data();
+    for (int64_t i = 0; i < n; i++) {
+        const f3 p = V(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]);
+        via_table[i] = texture_tile(w, p);
+        via_noise[i] = texture_tile(wn, p);
+    }
+}
+
 // sky_exit: 1 = World::ytop from the bricks (world_top_y over every brick, as k_world_top), the
 // frame kernels' traversal; 0 = ytop = Y, the reference's step counts.
 static int trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,

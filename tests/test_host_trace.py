@@ -92,6 +92,38 @@ def test_simplex3d_equals_oracle(host_lib):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+def test_texture_tile_table_equals_noise(host_lib):
+    """World::tex (rv_device.h tex_index / tex_table_entry, built once per context by k_tex_table)
+    gives the atlas tile sampleTexture's noise picks (src/raytracing_functions.cu:41-54) for every
+    hit position: lattice points, faces (integral coordinates), the carry boundaries of the +121.3 /
+    +1321.3 / +721.5 offsets (fractions near 0.7 and 0.5), the world's far faces and outside
+    positions (the kernels then evaluate the noise)."""
+    rng = np.random.default_rng(5)
+    lx, ly, lz = 5, 4, 6
+    dims = np.array([32, 16, 64], np.float64)
+    n = 60000
+    p = rng.uniform(0, 1, (n, 3)) * dims
+    k = n // 6
+    p[:k] = np.floor(p[:k])                                          # lattice points
+    p[k:2 * k, 0] = np.floor(p[k:2 * k, 0])                          # face hits
+    fr = np.array([0.7, 0.7, 0.5])
+    for j in range(3):                                               # carry boundaries +- a few ulp
+        s = slice((2 + j) * k, (3 + j) * k)
+        base = np.floor(p[s]) + fr
+        p[s] = np.nextafter(base.astype(np.float32), rng.choice([-np.inf, np.inf], base.shape)).astype(np.float64)
+    p[5 * k:5 * k + 500] = dims - rng.uniform(0, 1e-4, (500, 3))     # the far faces
+    p[5 * k + 500:5 * k + 1000] = dims + rng.uniform(0, 3, (500, 3))  # outside: noise path
+    p[5 * k + 1000:5 * k + 1500] = -rng.uniform(0, 3, (500, 3))
+    pts = np.ascontiguousarray(p.astype(np.float32))
+    tab = np.empty(n, np.int32)
+    noi = np.empty(n, np.int32)
+    host_lib.rvh_texture_tiles.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
+                                           C.c_void_p]
+    host_lib.rvh_texture_tiles(lx, ly, lz, pts.ctypes.data, n, tab.ctypes.data, noi.ctypes.data)
+    assert np.array_equal(tab, noi)
+    assert len(np.unique(noi)) >= 3                                 # several tiles exercised
+
+
 @pytest.mark.parametrize("variant", ["g1", "g4", "g8", "g4_replay"])
 def test_sky_exit_keeps_every_hit(host_lib, oracle_world, variant):
     """The frame kernels' sky exit (World::ytop, rv_device.h trace): a ray
