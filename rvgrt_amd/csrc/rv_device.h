@@ -183,11 +183,11 @@ RV_HD void world_set_brick(World& w, const uint32_t* brick) {
     w.csdf = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(brick) + w.coff);
 }
 
-// The sun horizon (trace_sun's exit, horizon_column): one dword per brick column, index bx | bz << lbx,
-// stored right after the CSDF region in the same allocation (no extra kernel argument: its base is
-// the brick base + 2 coff).  UINT32_MAX everywhere = no sun exit.
+// The sun horizon (trace_sun's exit, horizon_column): one dword per 2x2-voxel column, index
+// (x >> 1) | (z >> 1) << (lbx + 2), stored right after the CSDF region in the same allocation (no extra
+// kernel argument: its base is the brick base + 2 coff).  UINT32_MAX everywhere = no sun exit.
 __host__ __device__ inline size_t horizon_byte(uint32_t coff) { return 2 * (size_t)coff; }
-__host__ __device__ inline size_t horizon_bytes(int X, int Z) { return (size_t)(X >> 3) * (size_t)(Z >> 3) * 4; }
+__host__ __device__ inline size_t horizon_bytes(int X, int Z) { return (size_t)(X >> 1) * (size_t)(Z >> 1) * 4; }
 
 // Brick storage.  RV_SPLIT_BRICKS=0: one 128-B record per 8^3 brick, 64 B of
 // bits then 64 B of CSDF (coff = 64).  RV_SPLIT_BRICKS=1: a bits region of
@@ -338,7 +338,7 @@ RV_HD uint32_t gi_texel(const LinearWorld& w, uint32_t idx) { return w.gi[idx]; 
 // GI grid (X/4 x Y/4 x Z/4, x fastest, power-of-two dims < 2^32 cells): log2 GX, log2 (GX * GY)
 RV_HD uint32_t horizon_at(const World& w, uint32_t x, uint32_t z) {
     const uint32_t* hz = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w.brick) + horizon_byte(w.coff));
-    return hz[(x >> 3) | ((z >> 3) << w.lbx)];
+    return hz[(x >> 1) | ((z >> 1) << (w.lbx + 2))];
 }
 RV_HD uint32_t horizon_at(const LinearWorld&, uint32_t, uint32_t) { return 0xFFFFFFFFu; }   // no sun exit
 
@@ -717,7 +717,7 @@ struct StepCount {  // per-trace work counters (algorithmic bytes)
 // RW: look-ahead groups by stop search + re-walk (default) or by the step-by-step replay with an
 // early exit (round 1-2; kept for A/B and checked bit-exact on the CPU, tests/test_host_trace.py).
 // Re-walk: C4 0.667 -> 0.631 ms, C3 0.282 -> 0.270 (profiles/r02/rewalk_ab.txt).
-// SUN (trace_sun): the ray's direction is the sun's, and World::horizon (when set) holds, per brick
+// SUN (trace_sun): the ray's direction is the sun's, and World::horizon (when set) holds, per 2x2-voxel
 // column, a height from which a ray toward the sun can no longer meet a solid voxel (the sun exit).
 template <bool COUNT, int G = RV_DDA_GROUP, bool REUSE = (RV_WORD_REUSE != 0), bool RW = (RV_DDA_REWALK != 0),
           bool SUN = false, class WV = World>
@@ -1045,39 +1045,64 @@ RV_HD Hit trace_sun(const WV& w, f3 cam, f3 dir, float dist_h, StepCount& sc) {
     return trace<COUNT, G, REUSE, (RV_DDA_REWALK != 0), (RV_SUN_HORIZON != 0), WV>(w, cam, dir, dist_h, sc);
 }
 
-// Sun horizon of brick column (bx, bz) (World::horizon, the sun exit).  A ray toward the sun (slope
-// k = rise per unit of horizontal travel > 0, horizontal direction (ux, uz)) that starts in this column
-// at a height y passes over column c' only after a horizontal travel h >= hmin(c'), at a height
-// >= y + k h; it can meet a solid voxel of c' only if that height is below top(c') + 2 (the margin of
-// the sky exit).  The column's samples q(t) = its centre + t (ux, uz), t = 0, 8, 16, ... cover the band
-// that rays from any point of the column sweep (a point of the ray is within 5.7 + 4 voxels of a
-// sample; the 5 x 5 brick columns around a sample reach >= 16 voxels out), and every column of a
-// sample's neighbourhood is >= t - 34 away horizontally.  Returns max over samples of
-// (top + 2 - k max(0, t - 34)), rounded up: at or above it the ray can only miss.  coltop = highest
-// solid row + 1 per brick column (0: empty).
-RV_HD uint32_t horizon_column(const uint32_t* coltop, int nbx, int nbz, int lbx, int bx, int bz, float ux, float uz,
-                              float k) {
-    float H = 0.0f;
-    const float cx = (float)bx * 8.0f + 4.0f, cz = (float)bz * 8.0f + 4.0f;
-    const float ext = 8.0f * (float)(nbx > nbz ? nbx : nbz) + 48.0f;
-    for (int i = 0;; i++) {
-        const float t = 8.0f * (float)i;
-        const float qx = cx + t * ux, qz = cz + t * uz;
-        if (qx < -48.0f || qz < -48.0f || qx > 8.0f * (float)nbx + 48.0f || qz > 8.0f * (float)nbz + 48.0f || t > 2.0f * ext)
-            break;
-        const int sx = (int)floorf(qx * 0.125f), sz = (int)floorf(qz * 0.125f);
-        uint32_t m = 0;
-        for (int dz = -2; dz <= 2; dz++)
-            for (int dx = -2; dx <= 2; dx++) {
-                const int x = sx + dx, z = sz + dz;
-                if (x < 0 || z < 0 || x >= nbx || z >= nbz) continue;
-                const uint32_t v = coltop[(uint32_t)x | ((uint32_t)z << lbx)];
-                m = v > m ? v : m;
+// Highest solid row + 1 of each 2x2-voxel sub-column of a brick (index px | pz << 2; 0: empty);
+// wd = the brick's 16 bit dwords, by its y index.  Dword (y >> 2) | z << 1 holds rows 4 (y >> 2) .. +3
+// of slice z, row (y & 3) in bits 8 (y & 3) + x.
+RV_HD void brick_subcolumn_tops(const uint32_t* wd, uint32_t by, uint32_t (&t)[16]) {
+    for (uint32_t p = 0; p < 16; p++) {
+        const uint32_t px = p & 3u, pz = p >> 2;
+        const uint32_t m = (3u << (2u * px)) * 0x01010101u;   // x pair 2px, 2px+1 in all four rows
+        uint32_t top = 0;
+        for (uint32_t hy = 0; hy < 2; hy++)
+            for (uint32_t dz = 0; dz < 2; dz++) {
+                const uint32_t v = wd[hy | ((2u * pz + dz) << 1)] & m;
+                if (v) {
+                    const uint32_t y = by * 8u + hy * 4u + ((31u - (uint32_t)__builtin_clz(v)) >> 3) + 1u;
+                    top = top > y ? top : y;
+                }
             }
-        if (m) {
-            const float h = (float)m + 2.0f - k * (t > 34.0f ? t - 34.0f : 0.0f);
-            H = h > H ? h : H;
+        t[p] = top;
+    }
+}
+
+// Sun horizon of the 2x2-voxel column (i, j) (World::horizon, the sun exit).  A ray toward the sun
+// (rise k per unit of horizontal travel > 0, horizontal unit direction u = (ux, uz), n = (-uz, ux))
+// that starts anywhere in this column, at a height >= y, meets a solid voxel of another 2x2 column w
+// only inside w's footprint, after a horizontal travel h >= max(0, d.u - 2R) (d = centre offset of w,
+// R = |ux| + |uz| bounds either square's extent along u and along n), so at a height >= y + k h, and
+// only if w lies in the band |d.n| <= 2R ahead (d.u >= -2R) and that height is below top(w) (the
+// highest solid row + 1 of w).  Returns max over such w of (top(w) + 2 - k h), rounded up: from there
+// the ray can only miss.  Every such w is found from the samples q(t) = centre + t u, t integer:
+// the w with t = round(d.u) lies within 0.5 + 2R (<= 3.33) of q(t) on each axis, in the 5 x 5 columns
+// scanned.  The scan stops once no later sample can raise the result (its columns have d.u >= t - 0.5
+// and top <= topmax) or has left the world.  coltop: top per 2x2 column, index i | j << lcx.
+RV_HD uint32_t horizon_column(const uint32_t* coltop, int ncx, int ncz, int lcx, int i, int j, float ux, float uz,
+                              float k, float topmax) {
+    const float R = fabsf(ux) + fabsf(uz), nx = -uz, nz = ux;
+    const float cx = 2.0f * (float)i + 1.0f, cz = 2.0f * (float)j + 1.0f;
+    const float wx = 2.0f * (float)ncx, wz = 2.0f * (float)ncz;
+    float H = 0.0f;
+    for (int s = (int)floorf(-2.0f * R - 0.5f);; s++) {
+        const float t = (float)s;
+        if (t - 0.5f - 2.0f * R > 0.0f && topmax + 2.0f - k * (t - 0.5f - 2.0f * R) <= H) break;
+        const float qx = cx + t * ux, qz = cz + t * uz;
+        if (qx < -4.0f || qz < -4.0f || qx > wx + 4.0f || qz > wz + 4.0f) {
+            if (t > 0.0f) break;
+            continue;
         }
+        const int b0x = (int)floorf((qx - 4.4f) * 0.5f), b0z = (int)floorf((qz - 4.4f) * 0.5f);
+        for (int bz = b0z; bz <= b0z + 4; bz++)
+            for (int bx = b0x; bx <= b0x + 4; bx++) {
+                if (bx < 0 || bz < 0 || bx >= ncx || bz >= ncz) continue;
+                const uint32_t top = coltop[(uint32_t)bx | ((uint32_t)bz << lcx)];
+                if (!top) continue;
+                const float dx = 2.0f * (float)bx + 1.0f - cx, dz = 2.0f * (float)bz + 1.0f - cz;
+                const float du = dx * ux + dz * uz, dn = dx * nx + dz * nz;
+                if (fabsf(dn) > 2.0f * R + 0.01f || du < -2.0f * R - 0.01f) continue;
+                const float h = du - 2.0f * R > 0.0f ? du - 2.0f * R : 0.0f;
+                const float v = (float)top + 2.0f - k * h;
+                H = v > H ? v : H;
+            }
     }
     return (uint32_t)ceilf(H);
 }

@@ -68,26 +68,29 @@ uint32_t world_ytop(const HostWorld& h) {
 }
 
 // World::horizon as rv_abi.cpp's world_top builds it for the sun direction `sun` (k_column_top +
-// k_horizon: the same horizon_column)
+// k_horizon: the same brick_subcolumn_tops and horizon_column, topmax = World::ytop)
 void world_horizon(HostWorld& h, const float* sun, std::vector<uint32_t>& coltop, std::vector<uint32_t>& hz) {
     World& w = h.w;
-    const int nbx = w.X >> 3, nbz = w.Z >> 3;
-    coltop.assign((size_t)nbx * nbz, 0u);
-    hz.assign((size_t)nbx * nbz, 0u);
+    const int ncx = w.X >> 1, ncz = w.Z >> 1, lcx = w.lbx + 2;
+    coltop.assign((size_t)ncx * ncz, 0u);
+    hz.assign((size_t)ncx * ncz, 0u);
     const uint64_t nb = ((uint64_t)w.X * w.Y * w.Z) / 512;
     for (uint64_t b = 0; b < nb; b++) {
         uint32_t bx, by, bz;
         brick_coords(w, b, bx, by, bz);
-        const uint32_t t = brick_top_y(&h.brick[bits_word_index(b, 0)], by);
-        uint32_t& c = coltop[bx | (bz << (uint32_t)w.lbx)];
-        c = t > c ? t : c;
+        uint32_t t[16];
+        brick_subcolumn_tops(&h.brick[bits_word_index(b, 0)], by, t);
+        for (uint32_t q = 0; q < 16; q++) {
+            uint32_t& c = coltop[(bx * 4u + (q & 3u)) | ((bz * 4u + (q >> 2)) << (uint32_t)lcx)];
+            c = t[q] > c ? t[q] : c;
+        }
     }
     const double hxz = std::sqrt((double)sun[0] * sun[0] + (double)sun[2] * sun[2]);
     const float k = (float)((double)sun[1] / hxz * (1.0 - 1e-3));
-    for (int bz = 0; bz < nbz; bz++)
-        for (int bx = 0; bx < nbx; bx++)
-            hz[(uint32_t)bx | ((uint32_t)bz << w.lbx)] = horizon_column(coltop.data(), nbx, nbz, w.lbx, bx, bz,
-                                                                        (float)(sun[0] / hxz), (float)(sun[2] / hxz), k);
+    for (int j = 0; j < ncz; j++)
+        for (int i = 0; i < ncx; i++)
+            hz[(uint32_t)i | ((uint32_t)j << lcx)] = horizon_column(coltop.data(), ncx, ncz, lcx, i, j, (float)(sun[0] / hxz),
+                                                                    (float)(sun[2] / hxz), k, (float)w.ytop);
     std::copy(hz.begin(), hz.end(), h.brick.begin() + (long)(horizon_byte(w.coff) / 4));   // where horizon_at reads
 }
 

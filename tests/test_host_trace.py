@@ -168,7 +168,7 @@ def test_sky_exit_keeps_every_hit(host_lib, oracle_world, variant):
 @pytest.mark.parametrize("g8", [0, 1])
 @pytest.mark.parametrize("sky", ["cut", "full"])
 def test_sun_exit_keeps_every_shadow_hit(host_lib, oracle_world, g8, sky):
-    """The shadow rays' sun exit (trace_sun with World::horizon, built per brick
+    """The shadow rays' sun exit (trace_sun with World::horizon, built per 2x2-voxel
     column from the column tops for the sun direction, rv_device.h
     horizon_column): a ray toward the sun stops as a miss once it is above its
     column's horizon.  Shadow rays from the voxel surfaces (as the pre-pass,
@@ -197,7 +197,7 @@ def test_sun_exit_keeps_every_shadow_hit(host_lib, oracle_world, g8, sky):
     dist = np.zeros(len(org), np.float32)
     dirs = np.ascontiguousarray(np.broadcast_to(sun, org.shape), np.float32)
     g = np.zeros(len(org), HIT)
-    hz = np.zeros((ow.Z // 8) * (ow.X // 8), np.uint32)
+    hz = np.zeros((ow.Z // 2) * (ow.X // 2), np.uint32)
     p = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
     assert L.rvh_trace_sun(g8, ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(sun), p(org), p(dist), len(org), p(g),
                            p(hz)) == 0
