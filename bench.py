@@ -117,9 +117,14 @@ def main():
                          "that many frames per launch (the group's tail is shared by its frames; its RCCL "
                          "gather overlaps the next group); the Python loop puts frame k on stream k %% n; "
                          "1 = one frame at a time")
-    ap.add_argument("--loop", default="native", choices=["native", "python"],
-                    help="frame loop: rv_render_frames (C++: slots, streams, RCCL gather, untile) or the "
-                         "per-frame Python loop over the same library calls (torch.distributed gather)")
+    ap.add_argument("--loop", default="native", choices=["native", "python", "drawcuda"],
+                    help="frame loop: rv_render_frames (C++: slots, streams, RCCL gather, untile), the "
+                         "per-frame Python loop over the same library calls (torch.distributed gather), or "
+                         "drawcuda: renderLoop's own calls, rv_update_gi_data then rv_draw_cuda, one frame per "
+                         "call and no knowledge of the next camera (the drop-in path, src/main.cpp:119-132)")
+    ap.add_argument("--flow", type=int, default=1,
+                    help="python/drawcuda loops: one k_ref_flow launch per frame (rv_set_flow; 0 = drawCUDA's "
+                         "two launches with the GI update on the side stream)")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
     args = ap.parse_args()
@@ -183,6 +188,10 @@ def main():
     streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.stream_priority) for _ in range(nfl - 1)]
     r.set_gi_async(args.gi_async)
     r.set_pipeline(args.pipe)
+    r.set_flow(args.flow)
+    drawcuda = args.loop == "drawcuda"
+    if drawcuda and world_size > 1:
+        raise SystemExit("--loop drawcuda is the one-GPU drop-in loop")
     # Grouped reference frames (rv_set_frame_group) when a rank's render part is latency-bound (<= 48 K
     # waves of 64 pixels, as the latency-mode pipelined variant): the group's frames share one tail.
     # tools/shard_probe.py / tools/r03_ab.sh (profiles/r03/), 64-px tiles: C3 on one GPU 0.2234 -> 0.2063 ms
@@ -233,7 +242,8 @@ def main():
     for i in census:
         d = path[i]
         r.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time,
-                jx=d.jitter_x, jy=d.jitter_y, flags=flags | rv.RV_F_STATS)
+                jx=d.jitter_x, jy=d.jitter_y,
+                flags=flags | rv.RV_F_STATS | (rv.RV_F_REF_FETCH if drawcuda else 0))
 
     def mean_stats(st):
         return {k: int(round(v / len(census))) for k, v in st.items()}
@@ -349,6 +359,15 @@ def main():
         k = frame_no[0]
         frame_no[0] += 1
         s = streams[0] if serial[0] else streams[k % nfl]
+        if drawcuda:   # renderLoop (src/main.cpp:119-132): UpdateGIData, then drawCUDA of this frame's camera
+            d = take(1)[0][0]
+            r.set_stream(s.cuda_stream)
+            if gi_per_frame:
+                r.update_gi_data()
+            c = d.cam   # ref_compat drawCUDA: time <- jitterY argument (src/StateRender.cu:15-29)
+            r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(d.vp),
+                        np.ctypeslib.as_array(d.prev_vp), jitter_x=0.0, jitter_y=d.time)
+            return
         fa, fk = frame_args()
         if world_size == 1:
             r.set_stream(s.cuda_stream)
@@ -406,6 +425,10 @@ def main():
     # pipelined reference frames: every launch is k_ref_pipe (timed as stage "primary"); with N > 1
     # ranks a rank's launch holds its tiles and 1/N of the GI update's cells
     piped = native and args.path == "fused" and args.pipe and gi_per_frame and bool(flags & rv.RV_F_PREPASS)
+    # flow frames (the per-frame loops): every frame is one k_ref_flow launch (stage "primary") holding
+    # its pre-pass, its render and the next UpdateGIData's cells
+    flowed = (not native and world_size == 1 and args.flow and args.path == "fused" and nfl == 1
+              and bool(flags & rv.RV_F_PREPASS))
     gi_groups = grouped and gi_per_frame and bool(flags & rv.RV_F_PREPASS) and world_size == 1 and not piped
     fpl = nfl if (grouped and not gi_per_frame) else 1
     # grouped reference frames: the effective group size (the library caps it by the GI grid)
@@ -436,13 +459,18 @@ def main():
         elapsed = float(t.item())
 
     # single-frame latency: one frame per call, submitted and waited for alone (median of 9)
+    # (the per-frame loops: the frame's UpdateGIData + drawCUDA calls from an idle device to completion)
     lat = []
-    if native:
+    if native or world_size == 1:
         for _ in range(9):
             barrier()
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
-            run_native(1)
+            if native:
+                run_native(1)
+            else:
+                step()
+                drain()
             torch.cuda.synchronize(dev)
             lat.append((time.perf_counter() - t1) * 1000.0)
     latency_ms = round(float(np.median(lat)), 4) if lat else None
@@ -473,7 +501,7 @@ def main():
     dom = max((k for k in frame_stage_ms if k != "gi"), key=lambda k: frame_stage_ms[k])
     kernel_names = {"pp_primary": "k_prepass" if megakernel else "k_wf_pp_primary",
                     "pp_shadow": "k_wf_pp_shadow",
-                    "primary": ("k_ref_group" if ref_group else "k_ref_pipe" if piped else
+                    "primary": ("k_ref_group" if ref_group else "k_ref_pipe" if piped else "k_ref_flow" if flowed else
                                 "k_render_tiles" if world_size > 1 else "k_render")
                     if megakernel else "k_wf_primary",
                     "shadow": "k_wf_shadow",
@@ -481,7 +509,7 @@ def main():
     dom_ms = avg_stage_ms[dom]
     dom_fpl = stage_fpl[dom]
     dom_bytes = stage_bytes[dom] * dom_fpl
-    if piped and dom == "primary":   # the launch also runs the next frame's pre-pass and GI update
+    if (piped or flowed) and dom == "primary":   # the launch also runs a pre-pass and a GI update
         # (grouped: the next group's pre-pass and phase A of the group after; phase B's combine is a
         # separate small kernel, not counted here)
         dom_bytes = (stage_bytes["primary"] + stage_bytes["pp_primary"] + stage_bytes.get("gi", 0)) * dom_fpl
@@ -500,7 +528,7 @@ def main():
             traffic = None
     g = st_stage[dom]        # counters of the dominant stage's launch (census frame)
     gathers = (g["sphere_steps"] + g["dda_steps"] + g["csdf_checks"] + 2 * g["cone_steps"]) * dom_fpl
-    if piped and dom == "primary":
+    if (piped or flowed) and dom == "primary":
         for h in (st_stage["pp_primary"], gi_stats):
             gathers += (h["sphere_steps"] + h["dda_steps"] + h["csdf_checks"]) * dom_fpl
     if world_size > 1:
@@ -559,6 +587,7 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in avg_stage_ms.items()},   # per launch
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
             "pipelined": bool(piped),
+            "flow": bool(flowed),
             "frame_group": ref_group,
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,

@@ -138,3 +138,44 @@ def study(lg, sweeps, W, H, flags, pose, atlas, variants=VARIANTS):
         out[name] = compare(ref, render(w, build, tu, pu, W, H, flags, cam), dirs)
     wd = {b: world_diff(base_world, w) for b, w in worlds.items()}
     return wd, out
+
+
+def gi_cells_diff(wa, wb):
+    return int((wa.gi.reshape(-1, 4) != wb.gi.reshape(-1, 4)).any(axis=1).sum())
+
+
+def long_gi_sequence(lg, sweeps, frames, W, H, flags, pose, atlas, builds=("fma_gcc", "fma_clang"),
+                     render_at=None, rays=262144):
+    """The GI feedback loop under the reference's arithmetic: the reference
+    runs UpdateGIData before every drawCUDA, forever (src/main.cpp:119-132),
+    and every update reads the grid the previous ones wrote -- the bounce hit's
+    GI texel and the cell's own old value (src/CoarseArray.cu:315-354) -- so a
+    cell that a contracted build computes differently can spread.  Each build
+    (plain, and the contraction emulations) builds its own world and runs
+    `frames` rolling RAYPS windows (frame numbers 0.., the offset of
+    src/CoarseArray.cu:392-394) on it; after every update the GI cells that
+    differ from the plain build's grid are counted, and at the frames in
+    `render_at` (default: the last) each build renders the same camera on its
+    own grid and is compared with the plain render (compare()).  Returns one
+    record per frame."""
+    pos, yaw, pitch = pose
+    cam = O.camera_from_pose(pos, yaw, pitch, W, H)
+    worlds = {"plain": build_world("plain", lg, sweeps, atlas)}
+    for b in builds:
+        worlds[b] = build_world(b, lg, sweeps, atlas)
+    n = len(worlds["plain"].gi) // 4
+    render_at = set(render_at) if render_at else {frames}
+    dirs = pixel_dirs(cam, W, H)
+    off, curve = 0, []
+    for k in range(1, frames + 1):
+        cnt = min(rays, n - off)
+        for b, w in worlds.items():
+            with O.numerics(b):
+                w.gi_update(k - 1, first=off, count=cnt)
+        off = 0 if off + rays >= n else off + rays
+        rec = {"frame": k, "gi_cells": n, "gi_cells_diff": {b: gi_cells_diff(worlds["plain"], worlds[b]) for b in builds}}
+        if k in render_at:
+            ref = render(worlds["plain"], "plain", 0, 0, W, H, flags, cam)
+            rec["render"] = {b: compare(ref, render(worlds[b], b, 0, 0, W, H, flags, cam), dirs) for b in builds}
+        curve.append(rec)
+    return curve

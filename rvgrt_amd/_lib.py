@@ -79,6 +79,9 @@ SIGNATURES = [
     ("rv_set_pipeline", I32, [P, I32]),
     ("rv_set_frame_group", I32, [P, I32]),
     ("rv_get_frame_group", I32, [P, C.POINTER(C.c_int32)]),
+    ("rv_set_flow", I32, [P, I32]),
+    ("rv_tex_table_info", I32, [P, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]),
+    ("rv_flow_info", I32, [P, C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rv_set_gi_stats", I32, [P, I32]),
     ("rv_set_frames_in_flight", I32, [P, I32]),
     ("rv_world_build", I32, [P]),

@@ -83,6 +83,7 @@ struct rv_ctx {
     size_t gi_bytes = 0;
     uint32_t* atlas = nullptr;
     uint32_t* tex = nullptr;      // sampleTexture's tile table (World::tex), or null
+    bool tex_tried = false;       // tex_table() ran (the table is built once per context)
     // frame images (library-owned unless bound)
     uint32_t* color = nullptr; size_t color_pitch = 0; bool color_ext = false;
     uint32_t* mv = nullptr; size_t mv_pitch = 0; bool mv_ext = false;
@@ -166,6 +167,24 @@ struct rv_ctx {
     uint64_t carry_chunk = 0; int carry_n = 0, carry_r = 0, carry_half = 0;
     float carry_key[24] = {};
     int pipe_carry = 1;            // RV_PIPE_CARRY
+    // Flow frames (rv_set_flow; rv_frame / rv_draw_cuda of a frame with the pre-pass): one k_ref_flow
+    // launch per frame.  Tile-major half-res hand-off buffer, per-tile flags, the launch epoch and the
+    // count of render waves that fell back to evaluating their window.
+    int flow = 1;
+    uint2* flow_half = nullptr; uint32_t* flow_flag = nullptr; size_t flow_tiles = 0;
+    uint32_t flow_epoch = 0;
+    unsigned long long* flow_fb = nullptr;
+    uint64_t flow_launches = 0;
+    uint32_t flow_spin = 16384;      // env RV_FLOW_SPIN: polls before a render wave evaluates its window
+    bool flow_force_fallback = false;   // env RV_FLOW_FORCE_FALLBACK=1 (tests): no wave waits, all evaluate
+    // The next UpdateGIData computed ahead by a flow launch (camera-independent): update `spec_fr` of
+    // [spec_first, + spec_count) in gi_tmp, valid while the world/GI version is spec_world; recorded
+    // on the launch's stream (ev_spec).  upd_since_frame: an UpdateGIData came since the last frame
+    // (the caller runs renderLoop's per-frame update, so the next one is worth computing ahead).
+    bool spec_gi = false;
+    uint32_t spec_fr = 0; uint64_t spec_first = 0, spec_count = 0, spec_world = 0;
+    hipEvent_t ev_spec = nullptr; hipStream_t spec_stream = nullptr;
+    bool upd_since_frame = false;
     // grouped reference frames (rv_set_frame_group): frame sets per group parity, phase-A records
     // (this rank's stage slots and the all-gathered ones, 3 groups each), the update ring, the
     // phase-B stream and the loop's events
@@ -362,22 +381,6 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
         hipMemcpy(c->atlas, grey.data(), grey.size() * 4, hipMemcpyHostToDevice);
     }
     c->cfg.atlas_rgba8 = nullptr;
-    // sampleTexture's tile table (World::tex, rv_device.h tex_index): 4 B per voxel, a function of the
-    // voxel coordinates only, so it is built once here.  Env RV_TEX_TABLE=0, or no memory for it,
-    // leaves the noise evaluation in the kernels (identical tiles).
-    const char* te = getenv("RV_TEX_TABLE");
-    if (!(te && te[0] == '0')) {
-        const size_t tb = (size_t)w.X * w.Y * w.Z * 4;
-        if (hipMalloc(&c->tex, tb) == hipSuccess) {
-            launch_tex_table(c->stream, c->tex, w);
-            if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
-                return cleanup_fail(RV_ERR_HIP, "tex table");
-            w.tex = c->tex;
-        } else {
-            c->tex = nullptr;
-            (void)hipGetLastError();
-        }
-    }
     // frame slot 0 (more with rv_set_frames_in_flight)
     int W = cfg->width, H = cfg->height;
     c->own_color_pitch = align256((size_t)W * 4);
@@ -393,6 +396,9 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
+    if (const char* e = getenv("RV_FLOW")) c->flow = atoi(e);
+    if (const char* e = getenv("RV_FLOW_SPIN")) c->flow_spin = (uint32_t)std::max(0, atoi(e));
+    if (const char* e = getenv("RV_FLOW_FORCE_FALLBACK")) c->flow_force_fallback = atoi(e) != 0;
     if (const char* e = getenv("RV_GROUP")) c->group = std::min(32, std::max(0, atoi(e)));
     if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
         if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
@@ -505,6 +511,8 @@ void rv_destroy(rv_ctx* c) {
     if (c->comm_stream) hipStreamDestroy(c->comm_stream);
     if (c->ev_loop) hipEventDestroy(c->ev_loop);
     if (c->ev_world) hipEventDestroy(c->ev_world);
+    hipFree(c->flow_half); hipFree(c->flow_flag); hipFree(c->flow_fb);
+    if (c->ev_spec) hipEventDestroy(c->ev_spec);
     hipFree(c->cam_dev);
     if (c->cam_host) hipHostFree(c->cam_host);
     if (c->cam_ev) hipEventDestroy(c->cam_ev);
@@ -631,6 +639,36 @@ rv_status rv_set_pipeline(rv_ctx* c, int32_t on) {
     return RV_OK;
 }
 
+rv_status rv_tex_table_info(rv_ctx* c, int32_t* active, uint64_t* bytes) {
+    if (!c) return RV_ERR_INVALID;
+    if (active) *active = c->tex != nullptr;
+    if (bytes) *bytes = c->tex ? (uint64_t)c->w.X * c->w.Y * c->w.Z * 4 : 0;
+    return RV_OK;
+}
+
+rv_status rv_set_flow(rv_ctx* c, int32_t on) {
+    if (!c) return RV_ERR_INVALID;
+    c->flow = on != 0;
+    c->spec_gi = false;
+    return RV_OK;
+}
+
+rv_status rv_flow_info(rv_ctx* c, int32_t* active, uint64_t* launches, uint64_t* fallbacks) {
+    if (!c) return RV_ERR_INVALID;
+    if (active) *active = c->flow;
+    if (launches) *launches = c->flow_launches;
+    if (fallbacks) {
+        *fallbacks = 0;
+        if (c->flow_fb) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            unsigned long long v = 0;
+            HIP_TRY(c, hipMemcpy(&v, c->flow_fb, 8, hipMemcpyDeviceToHost));
+            *fallbacks = v;
+        }
+    }
+    return RV_OK;
+}
+
 rv_status rv_set_frame_group(rv_ctx* c, int32_t n) {
     if (!c || n < 0 || n > 32) return RV_ERR_INVALID;
     c->group = n;
@@ -651,6 +689,39 @@ rv_status rv_sync(rv_ctx* c) {
     if (c->slots.size() > 1)
         for (const FrameSlot& sl : c->slots)
             if (sl.pending) HIP_TRY(c, hipEventSynchronize(sl.done));
+    return RV_OK;
+}
+
+// sampleTexture's tile table (World::tex, rv_device.h tex_index): 4 B per voxel, a function of the voxel
+// coordinates only, so it is built once, at the first world build or import (bench.py's world_build_s
+// includes it) and kept through rebuilds.  It is optional -- a context without it evaluates the noise in
+// the kernels, with identical tiles -- so it is only allocated when it leaves room: the memory this
+// context may still allocate (CSDF build scratch, the GI scratch grid, two grouped-frame sets of 32
+// frames, the pipelined loop's buffers) plus 1 GiB, and at most half the device's free memory (other
+// contexts on the GPU).  Env RV_TEX_TABLE=0: never; =1: whenever the allocation succeeds.
+static rv_status tex_table(rv_ctx* c) {
+    if (c->tex_tried) return RV_OK;
+    c->tex_tried = true;
+    const char* te = getenv("RV_TEX_TABLE");
+    if (te && te[0] == '0') return RV_OK;
+    const bool force = te && te[0] == '1';
+    const size_t tb = (size_t)c->w.X * c->w.Y * c->w.Z * 4;
+    if (!force) {
+        size_t fr = 0, total = 0;
+        HIP_TRY(c, hipMemGetInfo(&fr, &total));
+        const size_t W = (size_t)c->cfg.width, H = (size_t)c->cfg.height;
+        const size_t frame = (c->own_color_pitch + c->own_mv_pitch + c->own_depth_pitch) * H + W * H * 2;
+        const size_t later = n_csdf(c) * 2 + c->gi_bytes + 2 * 32 * frame + 8 * W * H + ((size_t)1 << 30);
+        if (tb + later > fr || tb > fr / 2) return RV_OK;
+    }
+    if (hipMalloc(&c->tex, tb) != hipSuccess) {
+        c->tex = nullptr;
+        (void)hipGetLastError();
+        return RV_OK;
+    }
+    launch_tex_table(c->stream, c->tex, c->w);
+    LAUNCH_CHECK(c);
+    c->w.tex = c->tex;
     return RV_OK;
 }
 
@@ -722,6 +793,7 @@ rv_status rv_world_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
     c->geom_ver++;
+    if (rv_status ts = tex_table(c)) return ts;
     launch_fill_bricks(c->stream, c->brick, current_world(c), c->cfg.seed_x, c->cfg.seed_z);
     LAUNCH_CHECK(c);
     if (rv_status ts = world_top(c)) return ts;
@@ -737,6 +809,7 @@ rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t byte
     if (!c || !host) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
     if (kind != RV_WORLD_GI) c->geom_ver++;
+    if (rv_status ts = tex_table(c)) return ts;
     if (kind == RV_WORLD_BITS) {
         if (bytes != n_bits_words(c) * 4) return fail(c, RV_ERR_INVALID, "bits size mismatch");
         uint32_t* d = nullptr;
@@ -847,8 +920,26 @@ rv_status rv_update_gi_data(rv_ctx* c) {
     uint64_t rays = c->cfg.gi_rays_per_frame, n = n_gi(c);
     const bool timed = c->timing_n < c->timing_cap;
     hipEvent_t* e = timed ? &c->ev[(size_t)EV_PER_FRAME * c->timing_n] : nullptr;
-    rv_status s = gi_update(c, c->gi_frame, c->gi_offset, rays, c->gi_async, timed ? e[NSTAGE] : nullptr,
-                            timed ? e[NSTAGE + 1] : nullptr);
+    c->upd_since_frame = true;
+    const uint64_t count = c->gi_offset < n ? std::min(rays, n - c->gi_offset) : 0;
+    rv_status s;
+    if (c->spec_gi && c->spec_world == c->world_ver && c->spec_fr == c->gi_frame && c->spec_first == c->gi_offset &&
+        c->spec_count == count && !c->gi_stats) {
+        // computed ahead by the last flow launch (reads the same grid, same cells and frame number):
+        // only its copy-back is left, after that launch
+        c->spec_gi = false;
+        if (c->spec_stream != c->stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_spec, 0));
+        if (rv_status ws = wait_all_frames(c)) return ws;
+        if (timed) HIP_TRY(c, hipEventRecord(e[NSTAGE], c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->gi + c->gi_offset, c->gi_tmp + c->gi_offset, count * 4, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        if (timed) HIP_TRY(c, hipEventRecord(e[NSTAGE + 1], c->stream));
+        s = mark_world(c);
+    } else {
+        c->spec_gi = false;
+        s = gi_update(c, c->gi_frame, c->gi_offset, rays, c->gi_async, timed ? e[NSTAGE] : nullptr,
+                      timed ? e[NSTAGE + 1] : nullptr);
+    }
     if (s != RV_OK) return s;
     if (timed) c->gi_timed[c->timing_n] = 1;
     c->gi_frame++;
@@ -1063,13 +1154,111 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles, int which = 3)
     return RV_OK;
 }
 
+// Flow frame (rv_set_flow, default on): the drop-in drawCUDA of a frame with the pre-pass as one
+// k_ref_flow launch on `stream` -- pre-pass k | the next UpdateGIData's cells | render k, the render
+// waves waiting per half-res tile for the pre-pass waves of the same launch (rv_kernels.hip), so the
+// pre-pass's long camera + shadow rays overlap the render instead of forming a launch of their own.
+// The GI part runs only while the caller updates the grid before every frame (renderLoop's
+// UpdateGIData -> drawCUDA, src/main.cpp:119-132): its window is the one rv_update_gi_data will
+// apply next, read from the grid this frame renders with; that call then only copies it back.
+static bool flow_eligible(const rv_ctx* c, const FrameParams& f) {
+    return c->flow && c->megakernel && c->slots.size() == 1 && (f.flags & RV_F_PREPASS) != 0 && f.hw > 0 && f.hh > 0;
+}
+
+static rv_status flow_frame(rv_ctx* c, FrameParams f) {
+    const uint32_t ntx = (uint32_t)(f.hw + 7) / 8, nty = (uint32_t)(f.hh + 7) / 8;
+    const size_t ntiles = (size_t)ntx * nty;
+    if (c->flow_tiles != ntiles || !c->flow_half) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        hipFree(c->flow_half); hipFree(c->flow_flag);
+        c->flow_half = nullptr; c->flow_flag = nullptr; c->flow_tiles = 0;
+        HIP_TRY(c, hipMalloc(&c->flow_half, ntiles * 64 * sizeof(uint2)));
+        HIP_TRY(c, hipMalloc(&c->flow_flag, ntiles * 4));
+        HIP_TRY(c, hipMemset(c->flow_flag, 0, ntiles * 4));
+        c->flow_tiles = ntiles;
+        c->flow_epoch = 0;
+    }
+    if (!c->flow_fb) {
+        HIP_TRY(c, hipMalloc(&c->flow_fb, 8));
+        HIP_TRY(c, hipMemset(c->flow_fb, 0, 8));
+    }
+    if (++c->flow_epoch == 0) {   // 2^32 launches: restart the epochs from zeroed flags
+        HIP_TRY(c, hipMemsetAsync(c->flow_flag, 0, ntiles * 4, c->stream));
+        c->flow_epoch = 1;
+    }
+    const bool stats = (f.flags & RV_F_STATS) != 0;
+    const uint64_t n = n_gi(c), rays = c->cfg.gi_rays_per_frame;
+    const uint64_t first = c->gi_offset, count = first < n ? std::min(rays, n - first) : 0;
+    const bool spec_valid = c->spec_gi && c->spec_world == c->world_ver && c->spec_fr == c->gi_frame &&
+                            c->spec_first == first && c->spec_count == count;
+    // a full sweep flips the double buffer instead (gi_update); stats frames keep their counters clean
+    const bool spec = c->upd_since_frame && !spec_valid && !stats && !c->gi_stats && count > 0 && count < n;
+    if (spec && !c->gi_tmp) HIP_TRY(c, hipMalloc(&c->gi_tmp, c->gi_bytes));
+    PipeParams p{};
+    p.gi_prev = c->gi;
+    if (spec) {
+        p.gi_frame = c->gi_frame; p.gi_first = first; p.gi_count = count;
+        p.gi_next = c->gi_tmp + first;
+        c->carry_gi = false;   // the pipelined loop's kept update shares gi_tmp
+    }
+    p.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
+    p.gi_counters = c->counters + (size_t)ST_GI * NCNT;
+    f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
+    p.part[0] = PIPE_PP; p.part[1] = PIPE_GI; p.part[2] = PIPE_RENDER;
+    p.len[0] = pipe_len(f, PIPE_PP, 0);
+    p.len[1] = spec ? pipe_len(f, PIPE_GI, count) : 0u;
+    p.len[2] = pipe_len(f, PIPE_RENDER, 0);
+    p.flow_half = c->flow_half; p.flow_flag = c->flow_flag;
+    p.flow_epoch = c->flow_epoch; p.flow_ntx = ntx;
+    p.flow_expect = c->flow_force_fallback ? ~c->flow_epoch : c->flow_epoch;
+    p.flow_spin = c->flow_spin;
+    p.flow_fallback = c->flow_fb;
+    const bool timed = c->timing_n < c->timing_cap;
+    const size_t e0 = (size_t)EV_PER_FRAME * c->timing_n;
+    if (timed) { c->ev_stage[e0] = ST_PRIMARY; HIP_TRY(c, hipEventRecord(c->ev[e0], c->stream)); }
+    launch_ref_flow(c->stream, current_world(c), f, p);
+    LAUNCH_CHECK(c);
+    c->flow_launches++;
+    if (timed) {
+        c->ev_stage[e0 + 1] = -1;
+        HIP_TRY(c, hipEventRecord(c->ev[e0 + 1], c->stream));
+        c->ev_used[c->timing_n] = 2;
+        c->timing_n++;
+    }
+    if (spec) {
+        if (!c->ev_spec) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->ev_spec, c->stream));
+        c->spec_stream = c->stream;
+        c->spec_gi = true;
+        c->spec_fr = c->gi_frame; c->spec_first = first; c->spec_count = count; c->spec_world = c->world_ver;
+    }
+    if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
+        c->frames_since_order = 0;
+        launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
+                           n_chunks_pad(f.hw, f.hh));
+        launch_chunk_order(c->stream, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
+                           n_chunks_pad(f.W, f.H));
+        LAUNCH_CHECK(c);
+    }
+    return RV_OK;
+}
+
 rv_status rv_frame(rv_ctx* c, const rv_camera* cam, const float* vp16, const float* pvp16, float time,
                    float jx, float jy, int32_t flags) {
     if (!c || !cam) return RV_ERR_INVALID;
     if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_frame before rv_world_build/import");
     if (rv_status bs = begin_frame(c)) return bs;
     FrameParams f = make_params(c, cam, vp16, pvp16, time, jx, jy, flags);
-    if (rv_status rs = run_stages(c, f, false)) return rs;
+    const bool upd = c->upd_since_frame;
+    c->upd_since_frame = false;
+    if (flow_eligible(c, f)) {
+        c->upd_since_frame = upd;   // flow_frame reads it
+        rv_status fs = flow_frame(c, f);
+        c->upd_since_frame = false;
+        if (fs != RV_OK) return fs;
+    } else if (rv_status rs = run_stages(c, f, false)) {
+        return rs;
+    }
     return end_frame(c);
 }
 
@@ -1542,6 +1731,10 @@ struct rv_comm {
     hipEvent_t ready = nullptr, done = nullptr;
     uint64_t verified = 0;       // config record the ranks last agreed on (shard / bpp)
     bool aborted = false;
+    // verify_ranks' exchange buffers, allocated on first use and kept: (nranks + 1) x 8 B on the device
+    // (the all-gather's output, then this rank's hash), nranks x 8 B pinned on the host
+    uint64_t* vdev = nullptr;
+    uint64_t* vhost = nullptr;
 };
 
 static void comm_detach(rv_comm* m) { m->ctx = nullptr; }   // its context is being destroyed
@@ -2594,6 +2787,8 @@ void rv_comm_destroy(rv_comm* m) {
     }
     if (m->ready) hipEventDestroy(m->ready);
     if (m->done) hipEventDestroy(m->done);
+    if (m->vdev) hipFree(m->vdev);
+    if (m->vhost) hipHostFree(m->vhost);
     delete m;
 }
 
@@ -2668,7 +2863,7 @@ rv_status rv_set_gather_bpp(rv_ctx* c, int32_t bpp) {
 // order: a rank whose configuration changed after an agreed call and a rank
 // whose did not both enter it, see the disagreement and return
 // RV_ERR_INVALID before any tile or GI exchange is issued.
-static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
+static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags, int32_t gi_per_frame, int loop, int frames) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint64_t v) { for (int b = 0; b < 8; b++) { h ^= (v >> (8 * b)) & 255u; h *= 1099511628211ull; } };
     uint32_t w0;
@@ -2676,26 +2871,28 @@ static rv_status verify_ranks(rv_ctx* c, rv_comm* comm, int32_t flags) {
     mix((uint64_t)comm->nranks); mix((uint64_t)c->shard_n); mix((uint64_t)c->shard_px); mix((uint64_t)c->gather_bpp);
     mix(w0); mix((uint64_t)c->shard_max); mix((uint64_t)c->cfg.width); mix((uint64_t)c->cfg.height);
     mix((uint64_t)c->cfg.gi_rays_per_frame); mix((uint64_t)(flags & ~RV_F_STATS));
-    // the loop kind shapes the exchanges too (grouped frames: the group size)
-    mix((uint64_t)((flags & RV_F_STATS) ? 0 : group_frames(c))); mix((uint64_t)c->pipe);
+    // the loop the call takes (render_seq's own predicate: batched / grouped with its group size /
+    // pipelined / GI groups / per frame) and the frame count shape the sequence of collectives too
+    mix((uint64_t)loop); mix((uint64_t)gi_per_frame); mix((uint64_t)frames); mix((uint64_t)c->slots.size());
     for (int32_t t : c->shard_all) mix((uint64_t)(uint32_t)t);
     if (!c->comm_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-    uint64_t* d = nullptr;
-    HIP_TRY(c, hipMalloc(&d, 8 * (size_t)(comm->nranks + 1)));
-    std::vector<uint64_t> all((size_t)comm->nranks, 0);
+    const size_t nr = (size_t)comm->nranks;
+    if (!comm->vdev) HIP_TRY(c, hipMalloc(&comm->vdev, 8 * (nr + 1)));
+    if (!comm->vhost) HIP_TRY(c, hipHostMalloc(&comm->vhost, 8 * (nr + 1), hipHostMallocDefault));
+    // the pinned word holding this rank's hash is read by the upload below before the bounded wait returns
+    comm->vhost[nr] = h;
     rv_status st = RV_OK;
-    if (hipMemcpyAsync(d + comm->nranks, &h, 8, hipMemcpyHostToDevice, c->comm_stream) != hipSuccess)
+    if (hipMemcpyAsync(comm->vdev + nr, comm->vhost + nr, 8, hipMemcpyHostToDevice, c->comm_stream) != hipSuccess)
         st = fail(c, RV_ERR_HIP, "hipMemcpyAsync");
-    if (st == RV_OK) st = comm_all_gather(c, comm, d + comm->nranks, d, 8, c->comm_stream);
-    if (st == RV_OK && hipMemcpyAsync(all.data(), d, 8 * all.size(), hipMemcpyDeviceToHost, c->comm_stream) != hipSuccess)
+    if (st == RV_OK) st = comm_all_gather(c, comm, comm->vdev + nr, comm->vdev, 8, c->comm_stream);
+    if (st == RV_OK && hipMemcpyAsync(comm->vhost, comm->vdev, 8 * nr, hipMemcpyDeviceToHost, c->comm_stream) != hipSuccess)
         st = fail(c, RV_ERR_HIP, "hipMemcpyAsync");
     if (st == RV_OK) st = comm_wait_bounded(c, comm, comm_timeout_s());
-    hipFree(d);
     if (st != RV_OK) return st;
-    for (int r = 0; r < comm->nranks; r++)
-        if (all[(size_t)r] != h)
+    for (size_t r = 0; r < nr; r++)
+        if (comm->vhost[r] != h)
             return fail(c, RV_ERR_INVALID, "ranks disagree on the shard / deal weight / gather packing / frame config "
-                                            "(rank " + std::to_string(r) + ")");
+                                            "/ loop (rank " + std::to_string(r) + ")");
     comm->verified = h;
     return RV_OK;
 }
@@ -2707,7 +2904,14 @@ static rv_status render_seq(rv_ctx* c, const Seq& q, int32_t flags, int32_t gi_p
         // detaches only that one, rv_sync / rv_destroy wait on it)
         if (comm->ctx != c) return fail(c, RV_ERR_INVALID, "communicator was created on another context");
         c->comm_attached = comm;
-        if (rv_status vs = verify_ranks(c, comm, flags)) return vs;
+        // the loop this call takes: the same predicates as below
+        const int ns = (int)c->slots.size(), gF0 = group_frames(c);
+        const bool ref = gi_per_frame && (flags & RV_F_PREPASS) && c->megakernel && frames > 0;
+        const int loop = (!gi_per_frame && ns > 1 && c->megakernel && frames > 0) ? 1
+                         : (ref && c->pipe && gF0 >= 2 && !(flags & RV_F_STATS)) ? 100 + gF0
+                         : (ref && c->pipe) ? 2
+                         : (ref && c->shard_n == 0 && ns > 1) ? 3 : 0;
+        if (rv_status vs = verify_ranks(c, comm, flags, gi_per_frame, loop, frames)) return vs;
     }
     if (!c->world_ready) return fail(c, RV_ERR_STATE, "rv_render_frames before world");
     if (comm && (c->shard_n != comm->nranks || c->shard_rank != comm->rank))

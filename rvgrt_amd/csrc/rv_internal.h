@@ -107,6 +107,16 @@ struct PipeParams {
     unsigned long long* pp_counters;
     unsigned long long* gi_counters;
     uint32_t* wave_max;     // diagnostics (env RV_PIPE_WAVE_STATS): per workgroup, part << 30 | 10-ns ticks
+    // flow launch (launch_ref_flow, the drop-in drawCUDA): pre-pass k | GI update k+1 | render k of ONE
+    // camera.  Pre-pass wave t publishes its 8x8 half-res texels {dist, shadow} to flow_half[t * 64 ..]
+    // (tile-major, write-through) and then flow_flag[t] = flow_epoch; a render wave polls the flags of
+    // the <= 2x2 tiles under its half-res window, then reads them.  flow_ntx = tiles per half-res row.
+    uint2* flow_half;
+    uint32_t* flow_flag;
+    uint32_t flow_epoch, flow_ntx;
+    uint32_t flow_expect;   // the flag value a render wave waits for (== flow_epoch; tests: never published)
+    uint32_t flow_spin;     // polls before a render wave evaluates its window itself (~0.2 us each)
+    unsigned long long* flow_fallback;   // render waves that stopped waiting and computed their window
 };
 
 // Grouped reference frames (rv_set_frame_group): one launch
@@ -169,6 +179,8 @@ void launch_render(hipStream_t s, const World& w, const FrameParams& f);
 // workgroups of each part of a pipelined launch; then the launch itself
 uint32_t pipe_len(const FrameParams& f, int part, uint64_t gi_count);
 void launch_ref_pipe(hipStream_t s, const World& w, const FrameParams& f, const PipeParams& p);
+// flow launch: parts in the fixed order pre-pass (len[0]), GI (len[1]), render (len[2]) of f's camera
+void launch_ref_flow(hipStream_t s, const World& w, const FrameParams& f, const PipeParams& p);
 // grouped reference frames: the launch (GroupParams) and the GI update's phase B over one window
 // (cells [first, first + count) of GI frame `frame`, records rec[((q / chunk) * nwin + j) * chunk
 // + q % chunk] for cell first + q; output to ring position (dpos + q) & w.cmask) and the

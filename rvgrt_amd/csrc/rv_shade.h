@@ -40,10 +40,11 @@
 
 namespace rv {
 
-// one half-res pixel of distApproximationKernel (StateRender.cu:255-286)
+// one half-res pixel of distApproximationKernel (StateRender.cu:255-286): its distance (d - 8, the
+// value stored) and shadow texels
 template <bool STATS, class WV = World>
-__device__ __forceinline__ void prepass_pixel(const WV& w, const FrameParams& f, int ix, int iy,
-                                              uint32_t (&c)[NCNT]) {
+__device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, int ix, int iy,
+                                             uint32_t (&c)[NCNT], float& dist_out, float& shadow_out) {
     float x = ((float)ix + 0.5f) / (float)f.hw;
     float y = ((float)iy + 0.5f) / (float)f.hh;
     f3 dir = ray_dir(f, x, y);
@@ -60,7 +61,15 @@ __device__ __forceinline__ void prepass_pixel(const WV& w, const FrameParams& f,
         if (STATS) { c[CNT_TRACES]++; c[CNT_PP_SHADOW]++; }
     }
     if (STATS) { c[CNT_SPHERE] += sc.sphere; c[CNT_DDA] += sc.dda; c[CNT_CHECK] += sc.check; }
-    f.hdist[(size_t)iy * f.hw + ix] = d - 8.0f;
+    dist_out = d - 8.0f;
+    shadow_out = s;
+}
+template <bool STATS, class WV = World>
+__device__ __forceinline__ void prepass_pixel(const WV& w, const FrameParams& f, int ix, int iy,
+                                              uint32_t (&c)[NCNT]) {
+    float d, s;
+    prepass_eval<STATS, WV>(w, f, ix, iy, c, d, s);
+    f.hdist[(size_t)iy * f.hw + ix] = d;
     f.hshadow[(size_t)iy * f.hw + ix] = s;
 }
 

@@ -210,6 +210,22 @@ class StateRender:
         self._check(self._L.rv_get_frame_group(self._h, C.byref(v)), "rv_get_frame_group")
         return int(v.value)
 
+    def set_flow(self, on):
+        """rv_set_flow: drop-in frames as one launch (pre-pass | next GI window | render)."""
+        self._check(self._L.rv_set_flow(self._h, int(bool(on))), "rv_set_flow")
+
+    def flow_info(self):
+        """(active, launches, fallbacks) of the flow frames (rv_flow_info; synchronises)."""
+        a, n, fb = C.c_int32(), C.c_uint64(), C.c_uint64()
+        self._check(self._L.rv_flow_info(self._h, C.byref(a), C.byref(n), C.byref(fb)), "rv_flow_info")
+        return bool(a.value), int(n.value), int(fb.value)
+
+    def tex_table_info(self):
+        """(active, bytes) of sampleTexture's tile table (rv_tex_table_info)."""
+        a, n = C.c_int32(), C.c_uint64()
+        self._check(self._L.rv_tex_table_info(self._h, C.byref(a), C.byref(n)), "rv_tex_table_info")
+        return bool(a.value), int(n.value)
+
     def set_gi_stats(self, on):
         """rv_set_gi_stats: count the GI update's traversal steps (stage 'gi')."""
         self._check(self._L.rv_set_gi_stats(self._h, int(bool(on))), "rv_set_gi_stats")

@@ -15,8 +15,10 @@ size:
 * traversal: 20k random rays traced on the GPU and by the oracle on the
   exported world, bit-exact (32-bit brick offsets up to 2 GiB of records);
 * GI: a RAYPS-style partial update window, GPU vs oracle on the same grid;
-* frames: sampled rows of the config's frame (its resolution, flags and
-  pose), GPU vs oracle render of the same rows on the exported world.
+* frames: the config's whole frame (its resolution, flags and pose), GPU vs
+  oracle render on the exported world (RGBA8, MV and depth of every pixel;
+  the oracle renders a 4K reference frame in about a second on the box's
+  host threads).
 """
 import ctypes as C
 
@@ -103,8 +105,8 @@ def spread_rows(H, n, rng):
     return sorted(set(np.clip(rows, 0, H - 1).tolist()) | {0, H // 2, H - 1})
 
 
-def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=64):
-    """Sampled rows of the GPU frame against the oracle: RGBA8, MV and depth
+def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=64, pvp=None):
+    """Rows of the GPU frame (nrows spread rows; None: every row) against the oracle: RGBA8, MV and depth
     bit-exact (the HIP path computes the oracle's arithmetic: no contraction,
     correctly rounded division/sqrt; ocml's powf has matched glibc's on every
     pixel so far).  The tolerance of SURVEY s8c is for the reference's own
@@ -112,8 +114,8 @@ def check_rows(r, rv, oracle, ow, W, H, flags, cam_d, rng, time=0.0, nrows=64):
     img = r.readback(rv.RV_IMAGE_COLOR)
     mv = r.readback(rv.RV_IMAGE_MOTION)
     dep = r.readback(rv.RV_IMAGE_DEPTH)
-    fr = oracle.make_frame(W, H, flags, cam_d, time=time)
-    rows = spread_rows(H, nrows, rng)
+    fr = oracle.make_frame(W, H, flags, cam_d, time=time, pvp=pvp)
+    rows = list(range(H)) if nrows is None else spread_rows(H, nrows, rng)
     ref = oracle.render_rows(ow, fr, rows, want_stats=False)
     d = np.abs(img[rows].astype(np.int32) - ref["rgba"][rows].astype(np.int32)).max(axis=-1)
     print(f"{len(rows)} rows: {int((d > 0).sum())} of {d.size} pixels differ, max |d| {int(d.max())}")
@@ -168,7 +170,8 @@ def test_fullsize_world_traversal_gi_frame_rows(rv, atlas, oracle, cfgname, pose
     ow = check_world_rays_gi(r, rv, oracle, atlas, (lg,) * 3, lg, gi_window=cfg.gi_sweeps >= 0)
     cam, vp = rv.camera_from_pose(*pose_f32(cfg, pose), W, H)
     r.frame(cam, vp)
-    check_rows(r, rv, oracle, ow, W, H, cfg.flags, rv.camera_dict(cam, vp), np.random.default_rng(lg + 100))
+    # the whole frame: every pixel's RGBA8, MV and depth
+    check_rows(r, rv, oracle, ow, W, H, cfg.flags, rv.camera_dict(cam, vp), None, nrows=None)
     r.close()
 
 
@@ -217,9 +220,9 @@ def test_reference_native_config_draw_cuda(rv, atlas, oracle):
 def test_fullsize_pipelined_frames(rv, atlas, cfgname, grp):
     """The C3/C4 frame loop as bench.py runs it (pipelined launches: render
     k | GI update k+1 | pre-pass k+1; or grouped: 8 frames per launch) against UpdateGIData + drawCUDA one
-    frame at a time on the same full-size world: colour, depth and the GI
-    grid bit-identical after 6 frames (the one-at-a-time frames are checked
-    against the oracle by the tests above)."""
+    frame at a time (drawCUDA's two launches, rv_set_flow(0)) on the same full-size world: colour, depth
+    and the GI grid bit-identical after 6 frames (the one-at-a-time frames are checked against the oracle
+    by the tests above)."""
     from rvgrt_amd.configs import CONFIGS, pose_f32
     cfg = CONFIGS[cfgname]
     W, H = cfg.width, cfg.height
@@ -231,6 +234,7 @@ def test_fullsize_pipelined_frames(rv, atlas, cfgname, grp):
         for s in range(max(cfg.gi_sweeps, 0)):
             r.gi_update(s)
         r.set_pipeline(pipe)
+        r.set_flow(0)
         nf = 12 if grp else 6    # grouped: 8 frames per launch, the call ends mid-group
         if pipe:
             r.set_frame_group(grp)
@@ -245,5 +249,50 @@ def test_fullsize_pipelined_frames(rv, atlas, cfgname, grp):
     assert np.array_equal(a.readback(rv.RV_IMAGE_COLOR), b.readback(rv.RV_IMAGE_COLOR))
     assert np.array_equal(a.readback(rv.RV_IMAGE_DEPTH), b.readback(rv.RV_IMAGE_DEPTH))
     assert np.array_equal(a.world_export(rv.RV_WORLD_GI), b.world_export(rv.RV_WORLD_GI))
+    for r in rs:
+        r.close()
+
+
+@pytest.mark.parametrize("cfgname,pose", [("c3", "P0"), ("c4", "P0"), ("c4", "P1"), ("c5", "P0")])
+def test_fullsize_drop_in_flow_frames(rv, atlas, oracle, cfgname, pose):
+    """renderLoop's own calls at full size (UpdateGIData, then drawCUDA with a
+    moving camera, one frame per call, ref_compat): the flow launch (pre-pass k
+    | next window's GI cells | render k, render waves waiting per pre-pass tile)
+    against drawCUDA's two launches -- colour, motion, depth, half-res images
+    and the GI grid bit-identical after every frame, no render wave fell back
+    -- and the last frame whole against the oracle on the exported world."""
+    from rvgrt_amd.configs import CONFIGS, camera_path, pose_f32
+    cfg = CONFIGS[cfgname]
+    W, H = cfg.width, cfg.height
+    seq = camera_path(pose_f32(cfg, pose), W, H, 6, pan=0.002, ref_compat=True)
+    rs = []
+    for flow in (1, 0):
+        r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=atlas, ref_compat=True)
+        r.world_build()
+        for s in range(max(cfg.gi_sweeps, 0)):
+            r.gi_update(s)
+        r.set_flow(flow)
+        rs.append(r)
+    kinds = (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH, rv.RV_IMAGE_HALF_DIST, rv.RV_IMAGE_HALF_SHADOW)
+    for k in range(5):
+        d = seq[k]
+        c = d.cam
+        for r in rs:
+            r.update_gi_data()
+            r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(d.vp),
+                        np.ctypeslib.as_array(d.prev_vp), 0.0, d.time)
+        for kind in kinds:
+            assert np.array_equal(rs[0].readback(kind), rs[1].readback(kind)), (k, kind)
+        assert np.array_equal(rs[0].world_export(rv.RV_WORLD_GI), rs[1].world_export(rv.RV_WORLD_GI)), k
+    assert rs[0].flow_info()[1:] == (5, 0)
+    lg = cfg.log2_n
+    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas)
+    ow.bits[:] = rs[0].world_export(rv.RV_WORLD_BITS)
+    ow.csdf[:] = rs[0].world_export(rv.RV_WORLD_CSDF)
+    ow.gi[:] = rs[0].world_export(rv.RV_WORLD_GI)
+    d = seq[4]
+    check_rows(rs[0], rv, oracle, ow, W, H, cfg.flags | rv.RV_F_REF_FETCH,
+               rv.camera_dict(d.cam, np.ctypeslib.as_array(d.vp)), None, time=d.time, nrows=None,
+               pvp=np.ctypeslib.as_array(d.prev_vp))
     for r in rs:
         r.close()

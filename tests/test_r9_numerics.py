@@ -45,3 +45,22 @@ def test_study_builds_contract(oracle):
     for v in ("fma_gcc", "fma_clang"):
         with oracle.numerics(v) as L:
             assert L.or_numerics_contracted() == 1
+
+
+@pytest.mark.parametrize("pose", ["P0", "P1"])
+def test_tolerance_holds_after_64_gi_updates(study, atlas, pose):
+    """R9 over the GI feedback loop: 64 UpdateGIData frames (each a whole sweep
+    of the 32^3 grid: RAYPS 262144 >= its 32768 cells), every update reading
+    the grid the previous ones wrote, on worlds built and updated with the
+    contracted arithmetic; the reference frame rendered on each build's grid
+    after frame 64 stays within the SURVEY s8c tolerance of the plain oracle's
+    (profiles/r04/r9_long_gi.json has the per-frame curve at 128^3 and
+    256^3)."""
+    curve = study.long_gi_sequence(7, 1, 64, 320, 180, REF, TEST_POSES_128[pose], atlas, render_at=[1, 64])
+    assert len(curve) == 64
+    for b, m in curve[-1]["render"].items():
+        assert study.tolerance_ok(m), (pose, b, m)
+    # the contracted grids really differ (the loop is not vacuous) and the difference stays a small
+    # fraction of the grid
+    for b, nd in curve[-1]["gi_cells_diff"].items():
+        assert 0 < nd <= 0.05 * curve[-1]["gi_cells"], (b, nd)
