@@ -68,6 +68,28 @@ def algorithmic_bytes(st: dict, px: int, halfpx: int, prepass: bool, stage: str,
     return int(b)
 
 
+def binding_limit(tj: dict, launch_ms: float):
+    """What binds the profiled kernel, from its PMC summary (profiles/traffic_<config>.json, counters per
+    launch summed over the 8 XCDs; GRBM_GUI_ACTIVE is per XCD, so /8): the busy fraction of the 256
+    texture-data units (TD: the vector-memory return path of every gather), the VALU issue fraction (a
+    wave64 VALU instruction takes 2 cycles of a SIMD: 2 per CU-cycle on 4 SIMDs) and the HBM traffic
+    fraction of the 8 TB/s peak.  The largest names the limit."""
+    c = tj.get("counters_avg_per_launch", {})
+    cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    if cyc <= 0:
+        return None
+    td = c.get("TD_TD_BUSY_sum", 0.0) / (256.0 * cyc)
+    ta = c.get("TA_TA_BUSY_sum", 0.0) / (256.0 * cyc)
+    valu = c.get("SQ_INSTS_VALU", 0.0) / (2.0 * 256.0 * cyc)
+    hbm = tj.get("hbm_bytes_per_launch", 0) / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if launch_ms > 0 else 0.0
+    fr = {"td_busy": td, "valu_issue": valu, "hbm_traffic": hbm}
+    name = max(fr, key=fr.get)
+    label = {"td_busy": "vector-memory return path (TD busy)", "valu_issue": "VALU issue",
+             "hbm_traffic": "HBM bandwidth"}[name]
+    return {"name": label, "td_busy": round(td, 3), "ta_busy": round(ta, 3), "valu_issue": round(valu, 3),
+            "hbm_traffic": round(hbm, 3), "source": os.path.relpath(tj.get("_path", ""), ROOT) if tj.get("_path") else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -517,13 +539,16 @@ def main():
         dom_bytes = dom_bytes * len(my_tiles) / ntiles
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
+    limit = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}" + ("" if args.pose == "P0" else f"_{args.pose}")
-                         + ".json")
+                         + ("_drawcuda" if flowed else "") + ".json")
     if os.path.exists(tpath) and world_size == 1:   # PMC summaries are of the one-GPU launch
         try:
             tj = json.load(open(tpath))
+            tj["_path"] = tpath
             if tj.get("kernel", "").startswith(kernel_names[dom]) and tj.get("frames_per_launch", 1) == dom_fpl:
                 traffic = tj.get("hbm_bytes_per_launch")
+                limit = binding_limit(tj, dom_ms)
         except Exception:
             traffic = None
     g = st_stage[dom]        # counters of the dominant stage's launch (census frame)
@@ -534,7 +559,9 @@ def main():
     if world_size > 1:
         gathers = gathers * len(my_tiles) / ntiles
     gather_rate = gathers / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
-    roofline = {"bound": "hbm", "kernel": kernel_names[dom], "achieved": round(achieved, 2),
+    # "bound" names the axis the roofline is priced on (HBM bytes, the contract's hbm | mfma); what binds the
+    # kernel is `limit` (PMC): the vector-memory return path (TD busy) against VALU issue and HBM traffic
+    roofline = {"bound": "hbm", "limit": limit, "kernel": kernel_names[dom], "achieved": round(achieved, 2),
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
                 "avg_launch_ms": round(dom_ms, 4), "frames_per_launch": dom_fpl,

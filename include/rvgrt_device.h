@@ -28,7 +28,7 @@
  * the point / wrap / normalized-coordinate fetch of the reference's texture
  * descriptor (src/Texturepack.cu:105-111) exactly in arithmetic.
  *
- * The implementation is the library's traversal (rvgrt_amd/csrc/rv_device.h)
+ * The implementation is the library's traversal (include/rvgrt/rv_device.h)
  * instantiated on the reference layout; results are bit-identical with the
  * CPU oracle (tests/test_gpu_devapi.py).  Compile with -ffp-contract=off, as
  * the library is, for bit-exact results.
@@ -40,7 +40,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include "../rvgrt_amd/csrc/rv_device.h"
+#include "rvgrt/rv_device.h"
 
 #ifndef RVGRT_SHIX
 #define RVGRT_SHIX 12

@@ -32,14 +32,14 @@
  *
  * Launch as drawCUDA does: 8 x 8 blocks over W/2 x H/2 for distApproximationKernel, then over
  * W x H for renderKernel, on one stream.  The bodies are the library's own per-pixel code
- * (rvgrt_amd/csrc/rv_shade.h) on the reference layout: frames are bit-identical with the CPU
+ * (include/rvgrt/rv_shade.h) on the reference layout: frames are bit-identical with the CPU
  * oracle (tests/test_gpu_devapi.py).  Include in one translation unit (the __constant__
  * symbols are defined here); compile with -ffp-contract=off for bit-exact results.
  */
 #pragma once
 
 #include "rvgrt_device.h"
-#include "../rvgrt_amd/csrc/rv_shade.h"
+#include "rvgrt/rv_shade.h"
 
 /* half-res float images (the reference's cudaArrays behind its surface / texture objects) */
 struct rvgrtFloatSurf {

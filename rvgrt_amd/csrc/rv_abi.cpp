@@ -19,7 +19,7 @@
 #include <string>
 #include <vector>
 
-#include "rv_frame.h"
+#include "../../include/rvgrt/rv_frame.h"
 
 using namespace rv;
 

@@ -21,7 +21,7 @@
 // Queue order follows the wave ballots of the primary pass (8x8-pixel tiles),
 // so secondary rays stay spatially coherent; results are written per pixel,
 // so the (scheduling-dependent) queue order never changes the image.
-#include "rv_frame.h"
+#include "../../include/rvgrt/rv_frame.h"
 
 namespace rv {
 

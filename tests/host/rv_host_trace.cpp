@@ -1,5 +1,5 @@
 // rv_host_trace.cpp -- TEST INFRASTRUCTURE: the product's traversal source
-// (rvgrt_amd/csrc/rv_device.h, host+device functions) compiled for the CPU,
+// (include/rvgrt/rv_device.h, host+device functions) compiled for the CPU,
 // so tests/test_host_trace.py can check that exact code -- including its
 // compile-time variants (DDA look-ahead group, word reuse) -- against the oracle on
 // hosts without a GPU.  Not linked into librvgrt_hip.so and not used by it.
@@ -9,7 +9,7 @@
 #include <cmath>
 #include <vector>
 
-#include "../../rvgrt_amd/csrc/rv_device.h"
+#include "../../include/rvgrt/rv_device.h"
 
 using namespace rv;
 

@@ -1,4 +1,4 @@
-"""The product's traversal source (rvgrt_amd/csrc/rv_device.h) compiled for
+"""The product's traversal source (include/rvgrt/rv_device.h) compiled for
 the CPU (tests/host/rv_host_trace.cpp) against the oracle: hit, position,
 normal, uv and sphere/DDA/check step counts bit-exact on random rays, for
 every traversal variant the GPU kernels can select (DDA look-ahead group
