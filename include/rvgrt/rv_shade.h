@@ -153,18 +153,23 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
     if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER) && (RV_ABLATE & 4)) {
         color = sample_sky(dir, f.sun);
     } else if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER)) {
-        float nxw = fbm3D(hit.pos.x, hit.pos.z, f.time, 3, 0.06f, 2.0f, 0.6f);
-        float nyw = fbm3D(hit.pos.z, hit.pos.x, f.time + 112.0f, 3, 0.06f, 2.0f, 0.6f);
+        // timing ablations: 2048 the wave normal's two fbm3D, 8192 the reflection ray, 4096 its shadow ray
+        float nxw = (RV_ABLATE & 2048) ? 0.0f : fbm3D(hit.pos.x, hit.pos.z, f.time, 3, 0.06f, 2.0f, 0.6f);
+        float nyw = (RV_ABLATE & 2048) ? 0.0f : fbm3D(hit.pos.z, hit.pos.x, f.time + 112.0f, 3, 0.06f, 2.0f, 0.6f);
         f3 dn = normalize(add(hit.normal, V(nxw * 0.1f, nyw * 0.1f, 0.0f)));
         f3 rdir = reflect(dir, dn);
         RV_GD_KIND(gd::REFL);
-        Hit rh = trace<STATS, G, RE>(w, hit.pos, rdir, hround(0.001f), sc);
+        Hit rh;
+        if (RV_ABLATE & 8192) rh.hit = false;
+        else rh = trace<STATS, G, RE>(w, hit.pos, rdir, hround(0.001f), sc);
         if (STATS) { c[CNT_TRACES]++; c[CNT_REFL]++; }
         f3 rc;
         if (rh.hit) {
             rc = sample_texture(w, rh.u, rh.v, rh.pos);
             RV_GD_KIND(gd::REFL_SHADOW);
-            Hit rs = trace_sun<STATS, G, RE>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
+            Hit rs;
+            if (RV_ABLATE & 4096) rs.hit = false;
+            else rs = trace_sun<STATS, G, RE>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
             if (STATS) { c[CNT_TRACES]++; c[CNT_REFL_SHADOW]++; c[CNT_TEX]++; }
             if (rs.hit) rc = scale(rc, 0.1f);
         } else {

@@ -6,6 +6,8 @@ Writes profiles/r03/r9_numerics.json and prints a table.
 usage: python tools/r9_report.py [out.json]
        python tools/r9_report.py --long [out.json]   (the GI feedback loop over 64 UpdateGIData frames
                                                      -> profiles/r04/r9_long_gi.json)
+       python tools/r9_report.py --drift [frames]    (128^3 P0 for 1024 frames, rendered every 64
+                                                     -> profiles/r04/r9_long_gi_<frames>.json)
 """
 import json
 import os
@@ -65,7 +67,26 @@ def main_long(out_path):
         json.dump(report, f, indent=1)
 
 
+def main_drift(frames):
+    atlas = load_atlas()
+    t0 = time.time()
+    curve = S.long_gi_sequence(7, 1, frames, 320, 180, REF, TEST_POSES_128["P0"], atlas,
+                               render_at=list(range(64, frames + 1, 64)))
+    for rec in curve:
+        if "render" in rec:
+            print(rec["frame"], rec["gi_cells_diff"],
+                  {b: (round(m["rgba_exact"], 5), round(m["rgba_le2"], 5), m["hit_agree"]) for b, m in rec["render"].items()},
+                  flush=True)
+    out = os.path.join(ROOT, "profiles", "r04", f"r9_long_gi_{frames}.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump({"generator": "tools/r9_report.py --drift", "case": "128^3 320x180 reference P0", "curve": curve}, f)
+    print(f"done in {time.time() - t0:.0f} s")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--drift":
+        return main_drift(int(sys.argv[2]) if len(sys.argv) > 2 else 1024)
     if len(sys.argv) > 1 and sys.argv[1] == "--long":
         return main_long(sys.argv[2] if len(sys.argv) > 2 else
                          os.path.join(ROOT, "profiles", "r04", "r9_long_gi.json"))
