@@ -183,7 +183,7 @@ struct rv_ctx {
     // (the caller runs renderLoop's per-frame update, so the next one is worth computing ahead).
     bool spec_gi = false;
     uint32_t spec_fr = 0; uint64_t spec_first = 0, spec_count = 0, spec_world = 0;
-    hipEvent_t ev_spec = nullptr; hipStream_t spec_stream = nullptr;
+    hipEvent_t ev_spec = nullptr; hipStream_t spec_stream = nullptr; bool spec_rec = false;
     bool upd_since_frame = false;
     // grouped reference frames (rv_set_frame_group): frame sets per group parity, phase-A records
     // (this rank's stage slots and the all-gathered ones, 3 groups each), the update ring, the
@@ -890,6 +890,8 @@ static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t c
     if (c->slots.size() > 1)
         for (const FrameSlot& sl : c->slots)
             if (sl.pending && sl.submitted < c->gi_swapped_at) HIP_TRY(c, hipStreamWaitEvent(ks, sl.done, 0));
+    // a flow launch's GI part may still be writing gi_tmp (its cells for the next window)
+    if (c->spec_rec && c->spec_stream != ks) HIP_TRY(c, hipStreamWaitEvent(ks, c->ev_spec, 0));
     if (t0) HIP_TRY(c, hipEventRecord(t0, ks));
     launch_gi_update(ks, c->gi, c->gi_tmp, current_world(c), sun_dir(), frame, first, count,
                      c->counters + ST_GI * NCNT, c->gi_stats);
@@ -1229,6 +1231,7 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
         if (!c->ev_spec) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->ev_spec, c->stream));
         c->spec_stream = c->stream;
+        c->spec_rec = true;
         c->spec_gi = true;
         c->spec_fr = c->gi_frame; c->spec_first = first; c->spec_count = count; c->spec_world = c->world_ver;
     }
