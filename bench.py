@@ -615,6 +615,9 @@ def main():
             "path": args.path, "gi_async": bool(args.gi_async), "frames_in_flight": nfl,
             "pipelined": bool(piped),
             "flow": bool(flowed),
+            # render waves of the flow launches that stopped waiting for their pre-pass tiles and evaluated
+            # their half-res window themselves (rv_flow_info; 0 = every tile arrived through the hand-off)
+            "flow_fallbacks": r.flow_info()[2] if flowed else None,
             "frame_group": ref_group,
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,

@@ -42,7 +42,8 @@ namespace rv {
 
 // one half-res pixel of distApproximationKernel (StateRender.cu:255-286): its distance (d - 8, the
 // value stored) and shadow texels
-template <bool STATS, class WV = World>
+// G: the traversal's DDA look-ahead (every G gives the same hit: rv_device.h trace)
+template <bool STATS, class WV = World, int G = RV_G_PREPASS>
 __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, int ix, int iy,
                                              uint32_t (&c)[NCNT], float& dist_out, float& shadow_out) {
     float x = ((float)ix + 0.5f) / (float)f.hw;
@@ -50,13 +51,13 @@ __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, 
     f3 dir = ray_dir(f, x, y);
     StepCount sc{};
     RV_GD_KIND(gd::PP_PRIMARY);
-    Hit h = trace<STATS, RV_G_PREPASS, false>(w, f.pos, dir, 0.0f, sc);
+    Hit h = trace<STATS, G, false>(w, f.pos, dir, 0.0f, sc);
     float d = h.hit ? length(sub(h.pos, f.pos)) : 300.0f;
     float s = 1.0f;
     if (STATS) { c[CNT_TRACES]++; c[CNT_PP_PRIMARY]++; c[CNT_UNDEF] += h.undef; }
     if (h.hit && !(RV_ABLATE & 1024)) {
         RV_GD_KIND(gd::PP_SHADOW);
-        Hit sh = trace_sun<STATS, RV_G_PREPASS, false>(w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
+        Hit sh = trace_sun<STATS, G, false>(w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
         s = sh.hit ? SHADOW_HIT : 1.0f;
         if (STATS) { c[CNT_TRACES]++; c[CNT_PP_SHADOW]++; }
     }

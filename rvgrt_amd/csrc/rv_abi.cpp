@@ -171,12 +171,16 @@ struct rv_ctx {
     // launch per frame.  Tile-major half-res hand-off buffer, per-tile flags, the launch epoch and the
     // count of render waves that fell back to evaluating their window.
     int flow = 1;
-    uint2* flow_half = nullptr; uint32_t* flow_flag = nullptr; size_t flow_tiles = 0;
+    unsigned long long* flow_half = nullptr; size_t flow_tiles = 0;
     uint32_t flow_epoch = 0;
     unsigned long long* flow_fb = nullptr;
     uint64_t flow_launches = 0;
     uint32_t flow_spin = 16384;      // env RV_FLOW_SPIN: polls before a render wave evaluates its window
     bool flow_force_fallback = false;   // env RV_FLOW_FORCE_FALLBACK=1 (tests): no wave waits, all evaluate
+    // env RV_FLOW_PP_ORDER: 1 (default) pre-pass tiles in the render's chunk order, so the tiles the first
+    // render waves read are published first (C3 -2 %, C4 -0.2 %, render waves finding a tile unpublished
+    // on arrival 330 -> 130 per C4 frame: profiles/r04/flow_ab.txt); 0 the pre-pass's own cost order
+    uint32_t flow_pp_order = 1;
     // The next UpdateGIData computed ahead by a flow launch (camera-independent): update `spec_fr` of
     // [spec_first, + spec_count) in gi_tmp, valid while the world/GI version is spec_world; recorded
     // on the launch's stream (ev_spec).  upd_since_frame: an UpdateGIData came since the last frame
@@ -399,6 +403,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_FLOW")) c->flow = atoi(e);
     if (const char* e = getenv("RV_FLOW_SPIN")) c->flow_spin = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("RV_FLOW_FORCE_FALLBACK")) c->flow_force_fallback = atoi(e) != 0;
+    if (const char* e = getenv("RV_FLOW_PP_ORDER")) c->flow_pp_order = (uint32_t)(atoi(e) != 0);
     if (const char* e = getenv("RV_GROUP")) c->group = std::min(32, std::max(0, atoi(e)));
     if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
         if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
@@ -511,7 +516,7 @@ void rv_destroy(rv_ctx* c) {
     if (c->comm_stream) hipStreamDestroy(c->comm_stream);
     if (c->ev_loop) hipEventDestroy(c->ev_loop);
     if (c->ev_world) hipEventDestroy(c->ev_world);
-    hipFree(c->flow_half); hipFree(c->flow_flag); hipFree(c->flow_fb);
+    hipFree(c->flow_half); hipFree(c->flow_fb);
     if (c->ev_spec) hipEventDestroy(c->ev_spec);
     hipFree(c->cam_dev);
     if (c->cam_host) hipHostFree(c->cam_host);
@@ -1172,11 +1177,10 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     const size_t ntiles = (size_t)ntx * nty;
     if (c->flow_tiles != ntiles || !c->flow_half) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        hipFree(c->flow_half); hipFree(c->flow_flag);
-        c->flow_half = nullptr; c->flow_flag = nullptr; c->flow_tiles = 0;
-        HIP_TRY(c, hipMalloc(&c->flow_half, ntiles * 64 * sizeof(uint2)));
-        HIP_TRY(c, hipMalloc(&c->flow_flag, ntiles * 4));
-        HIP_TRY(c, hipMemset(c->flow_flag, 0, ntiles * 4));
+        hipFree(c->flow_half);
+        c->flow_half = nullptr; c->flow_tiles = 0;
+        HIP_TRY(c, hipMalloc(&c->flow_half, ntiles * 64 * 8));
+        HIP_TRY(c, hipMemset(c->flow_half, 0, ntiles * 64 * 8));   // tag 0: no launch's
         c->flow_tiles = ntiles;
         c->flow_epoch = 0;
     }
@@ -1184,8 +1188,8 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
         HIP_TRY(c, hipMalloc(&c->flow_fb, 8));
         HIP_TRY(c, hipMemset(c->flow_fb, 0, 8));
     }
-    if (++c->flow_epoch == 0) {   // 2^32 launches: restart the epochs from zeroed flags
-        HIP_TRY(c, hipMemsetAsync(c->flow_flag, 0, ntiles * 4, c->stream));
+    if (++c->flow_epoch > 0x7FFFFFFFu) {   // 31-bit tags: restart the epochs from a zeroed buffer
+        HIP_TRY(c, hipMemsetAsync(c->flow_half, 0, ntiles * 64 * 8, c->stream));
         c->flow_epoch = 1;
     }
     const bool stats = (f.flags & RV_F_STATS) != 0;
@@ -1207,12 +1211,14 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     p.gi_counters = c->counters + (size_t)ST_GI * NCNT;
     f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
     p.part[0] = PIPE_PP; p.part[1] = PIPE_GI; p.part[2] = PIPE_RENDER;
-    p.len[0] = pipe_len(f, PIPE_PP, 0);
+    p.flow_pp_by_render = c->flow_pp_order;
+    // pre-pass workgroups: 16 per render chunk slot in the render's order, or the pre-pass's own grid
+    p.len[0] = c->flow_pp_order ? n_chunks_pad(f.W, f.H) * 16u : pipe_len(f, PIPE_PP, 0);
     p.len[1] = spec ? pipe_len(f, PIPE_GI, count) : 0u;
     p.len[2] = pipe_len(f, PIPE_RENDER, 0);
-    p.flow_half = c->flow_half; p.flow_flag = c->flow_flag;
+    p.flow_half = c->flow_half;
     p.flow_epoch = c->flow_epoch; p.flow_ntx = ntx;
-    p.flow_expect = c->flow_force_fallback ? ~c->flow_epoch : c->flow_epoch;
+    p.flow_expect = c->flow_force_fallback ? c->flow_epoch ^ 0x40000000u : c->flow_epoch;
     p.flow_spin = c->flow_spin;
     p.flow_fallback = c->flow_fb;
     const bool timed = c->timing_n < c->timing_cap;
