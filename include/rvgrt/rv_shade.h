@@ -34,6 +34,9 @@
 #ifndef RV_CONES_BATCHED  // the six cones' first-step gathers issued together (trace_cones6)
 #define RV_CONES_BATCHED 1
 #endif
+#ifndef RV_G_REFL         // the water reflection ray's look-ahead (0: the frame's G); A/B builds
+#define RV_G_REFL 0
+#endif
 #ifndef RV_G_GI           // GI init / update
 #define RV_G_GI 4
 #endif
@@ -162,7 +165,7 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         RV_GD_KIND(gd::REFL);
         Hit rh;
         if (RV_ABLATE & 8192) rh.hit = false;
-        else rh = trace<STATS, G, RE>(w, hit.pos, rdir, hround(0.001f), sc);
+        else rh = trace<STATS, RV_G_REFL ? RV_G_REFL : G, RE>(w, hit.pos, rdir, hround(0.001f), sc);
         if (STATS) { c[CNT_TRACES]++; c[CNT_REFL]++; }
         f3 rc;
         if (rh.hit) {
