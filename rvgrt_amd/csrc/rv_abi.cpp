@@ -175,6 +175,7 @@ struct rv_ctx {
     uint32_t flow_epoch = 0;
     unsigned long long* flow_fb = nullptr;
     uint64_t flow_launches = 0;
+    int gi_pairs = 0;                // env RV_GI_PAIRS: latency-variant pipelined launches trace a GI cell's two rays on a lane pair
     uint32_t flow_spin = 16384;      // env RV_FLOW_SPIN: polls before a render wave evaluates its window
     bool flow_force_fallback = false;   // env RV_FLOW_FORCE_FALLBACK=1 (tests): no wave waits, all evaluate
     // env RV_FLOW_PP_ORDER: 1 (default) pre-pass tiles in the render's chunk order, so the tiles the first
@@ -401,6 +402,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
     if (const char* e = getenv("RV_FLOW")) c->flow = atoi(e);
+    if (const char* e = getenv("RV_GI_PAIRS")) c->gi_pairs = atoi(e);
     if (const char* e = getenv("RV_FLOW_SPIN")) c->flow_spin = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("RV_FLOW_FORCE_FALLBACK")) c->flow_force_fallback = atoi(e) != 0;
     if (const char* e = getenv("RV_FLOW_PP_ORDER")) c->flow_pp_order = (uint32_t)(atoi(e) != 0);
@@ -2169,8 +2171,11 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
         p.pp_hdist = c->pipe_half[half(k + 1)][0]; p.pp_hshadow = c->pipe_half[half(k + 1)][1];
         p.pp_counters = c->counters + (size_t)ST_PP_PRIMARY * NCNT;
         p.gi_counters = cnt_gi;
-        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, mine) : 0u, more ? pipe_len(f, PIPE_PP, 0) : 0u,
-                                  pipe_len(f, PIPE_RENDER, 0)};
+        // latency-variant launches (a rank's share from 4 ranks, C3) run the GI cells on lane pairs
+        const uint32_t rlen = pipe_len(f, PIPE_RENDER, 0);
+        p.gi_pairs = c->gi_pairs && pipe_latency_variant(f, rlen) ? 1u : 0u;
+        const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * mine : mine) : 0u,
+                                  more ? pipe_len(f, PIPE_PP, 0) : 0u, rlen};
         for (int i = 0; i < 3; i++) {
             p.part[i] = (c->pipe_order >> (4 * (2 - i))) & 0xFu;
             p.len[i] = lens[p.part[i]];

@@ -448,16 +448,19 @@ def test_render_frames_native_loop(rv, atlas, flags, T):
     ref.close()
 
 
-@pytest.mark.parametrize("order,rays", [("012", 5000), ("210", 5000), ("102", 5000), ("102", 4096), ("012", 2048)])
-def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order, rays):
+@pytest.mark.parametrize("order,rays,pairs", [("012", 5000, 0), ("210", 5000, 0), ("102", 5000, 0), ("102", 4096, 0),
+                                              ("012", 2048, 0), ("102", 5000, 1), ("102", 4096, 1)])
+def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order, rays, pairs):
     """rv_set_pipeline: render k | GI update k+1 | pre-pass k+1 in one launch.
     The frames and the GI grid equal UpdateGIData + drawCUDA one frame at a
     time, for every dispatch order of the parts, over a rolling GI window
     that wraps (5000-cell windows of a 32^3 grid: linear cell order, a partial
     last block; 4096 / 2048: whole planes, blocked cell order) -- and the
-    oracle agrees on the grid (bit-exact) and the last frame."""
+    oracle agrees on the grid (bit-exact) and the last frame.  pairs: the latency variant's GI cells on
+    lane pairs (RV_GI_PAIRS; this small frame's launches are latency-variant ones)."""
     from rvgrt_amd.configs import TEST_POSES_128
     monkeypatch.setenv("RV_PIPE_ORDER", order)
+    monkeypatch.setenv("RV_GI_PAIRS", str(pairs))
     lg, W, H = 7, 320, 192
     flags = rv.RV_FLAGS_REFERENCE
     cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
