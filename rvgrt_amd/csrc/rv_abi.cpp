@@ -175,7 +175,11 @@ struct rv_ctx {
     uint32_t flow_epoch = 0;
     unsigned long long* flow_fb = nullptr;
     uint64_t flow_launches = 0;
-    int gi_pairs = 0;                // env RV_GI_PAIRS: latency-variant pipelined launches trace a GI cell's two rays on a lane pair
+    // env RV_GI_PAIRS: latency-variant launches trace a GI cell's two rays on a lane pair (1 all, 0 none);
+    // default -1: a rank's tile share only -- its GI part is 1/N of the cells and its longest GI waves
+    // were the launch's floor (8-rank C4 share 137.4 -> 132.8 us/frame, GI longest wave 127.5 -> 98.9 us),
+    // while a whole C3 frame's GI waves double for no gain (0.204 -> 0.240 ms; profiles/r04/gi_pairs_ab.txt)
+    int gi_pairs = -1;
     uint32_t flow_spin = 16384;      // env RV_FLOW_SPIN: polls before a render wave evaluates its window
     bool flow_force_fallback = false;   // env RV_FLOW_FORCE_FALLBACK=1 (tests): no wave waits, all evaluate
     // env RV_FLOW_PP_ORDER: 1 (default) pre-pass tiles in the render's chunk order, so the tiles the first
@@ -1216,8 +1220,9 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     p.flow_pp_by_render = c->flow_pp_order;
     // pre-pass workgroups: 16 per render chunk slot in the render's order, or the pre-pass's own grid
     p.len[0] = c->flow_pp_order ? n_chunks_pad(f.W, f.H) * 16u : pipe_len(f, PIPE_PP, 0);
-    p.len[1] = spec ? pipe_len(f, PIPE_GI, count) : 0u;
     p.len[2] = pipe_len(f, PIPE_RENDER, 0);
+    p.gi_pairs = c->gi_pairs > 0 && pipe_latency_variant(f, p.len[2]) ? 1u : 0u;   // whole frames: off unless forced
+    p.len[1] = spec ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * count : count) : 0u;
     p.flow_half = c->flow_half;
     p.flow_epoch = c->flow_epoch; p.flow_ntx = ntx;
     p.flow_expect = c->flow_force_fallback ? c->flow_epoch ^ 0x40000000u : c->flow_epoch;
@@ -2173,7 +2178,7 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
         p.gi_counters = cnt_gi;
         // latency-variant launches (a rank's share from 4 ranks, C3) run the GI cells on lane pairs
         const uint32_t rlen = pipe_len(f, PIPE_RENDER, 0);
-        p.gi_pairs = c->gi_pairs && pipe_latency_variant(f, rlen) ? 1u : 0u;
+        p.gi_pairs = (c->gi_pairs > 0 || (c->gi_pairs < 0 && tiles)) && pipe_latency_variant(f, rlen) ? 1u : 0u;
         const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * mine : mine) : 0u,
                                   more ? pipe_len(f, PIPE_PP, 0) : 0u, rlen};
         for (int i = 0; i < 3; i++) {

@@ -42,16 +42,19 @@ def _images(r, rv):
                                            rv.RV_IMAGE_HALF_DIST, rv.RV_IMAGE_HALF_SHADOW)]
 
 
-@pytest.mark.parametrize("pose,rays,readback_every", [("P0", 5000, 1), ("P1", 5000, 4), ("P0", 4096, 3)])
-def test_flow_frames_equal_two_launches_and_oracle(rv, atlas, oracle, pose, rays, readback_every):
+@pytest.mark.parametrize("pose,rays,readback_every,pairs", [("P0", 5000, 1, 0), ("P1", 5000, 4, 0), ("P0", 4096, 3, 0),
+                                                            ("P1", 5000, 2, 1)])
+def test_flow_frames_equal_two_launches_and_oracle(rv, atlas, oracle, monkeypatch, pose, rays, readback_every, pairs):
     """renderLoop's calls with a moving camera (yaw pan, the jitter sequence as
     the frame time, previous VP per frame), over a rolling GI window that wraps
     the 32^3 grid: every image and the GI grid equal the two-launch path after
     every frame read back (reading back rarely leaves several frames queued
     behind each other); the grid equals the oracle's rolling updates and the
     last frame the oracle's render (RGBA8, MV, depth); no render wave had to
-    fall back to evaluating its own window."""
+    fall back to evaluating its own window.  pairs: the GI cells of these (latency-variant) launches on
+    lane pairs (RV_GI_PAIRS)."""
     from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    monkeypatch.setenv("RV_GI_PAIRS", str(pairs))
     lg, W, H = 7, 320, 192
     nfr = 11
     seq = camera_path(TEST_POSES_128[pose], W, H, nfr + 1, pan=0.02, ref_compat=True)
