@@ -180,6 +180,7 @@ struct rv_ctx {
     // were the launch's floor (8-rank C4 share 137.4 -> 132.8 us/frame, GI longest wave 127.5 -> 98.9 us),
     // while a whole C3 frame's GI waves double for no gain (0.204 -> 0.240 ms; profiles/r04/gi_pairs_ab.txt)
     int gi_pairs = -1;
+    uint32_t prio_blocks = 0;        // env RV_PRIO_BLOCKS: leading pipelined-launch workgroups per part at high issue priority
     uint32_t flow_spin = 16384;      // env RV_FLOW_SPIN: polls before a render wave evaluates its window
     bool flow_force_fallback = false;   // env RV_FLOW_FORCE_FALLBACK=1 (tests): no wave waits, all evaluate
     // env RV_FLOW_PP_ORDER: 1 (default) pre-pass tiles in the render's chunk order, so the tiles the first
@@ -407,6 +408,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
     if (const char* e = getenv("RV_FLOW")) c->flow = atoi(e);
     if (const char* e = getenv("RV_GI_PAIRS")) c->gi_pairs = atoi(e);
+    if (const char* e = getenv("RV_PRIO_BLOCKS")) c->prio_blocks = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("RV_FLOW_SPIN")) c->flow_spin = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("RV_FLOW_FORCE_FALLBACK")) c->flow_force_fallback = atoi(e) != 0;
     if (const char* e = getenv("RV_FLOW_PP_ORDER")) c->flow_pp_order = (uint32_t)(atoi(e) != 0);
@@ -2179,6 +2181,7 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
         // latency-variant launches (a rank's share from 4 ranks, C3) run the GI cells on lane pairs
         const uint32_t rlen = pipe_len(f, PIPE_RENDER, 0);
         p.gi_pairs = (c->gi_pairs > 0 || (c->gi_pairs < 0 && tiles)) && pipe_latency_variant(f, rlen) ? 1u : 0u;
+        p.prio_blocks = c->prio_blocks;
         const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * mine : mine) : 0u,
                                   more ? pipe_len(f, PIPE_PP, 0) : 0u, rlen};
         for (int i = 0; i < 3; i++) {
