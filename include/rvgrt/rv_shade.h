@@ -37,6 +37,12 @@
 #ifndef RV_G_REFL         // the water reflection ray's look-ahead (0: the frame's G); A/B builds
 #define RV_G_REFL 0
 #endif
+#ifndef RV_COL_REFL       // the water reflection's DDA skips the voxel gathers of groups above the terrain
+#define RV_COL_REFL 1     // (rv_device.h trace COL)
+#endif
+#ifndef RV_COL_GI         // ... the GI update's bounce rays too (A/B)
+#define RV_COL_GI 0
+#endif
 #ifndef RV_G_GI           // GI init / update
 #define RV_G_GI 4
 #endif
@@ -165,7 +171,11 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         RV_GD_KIND(gd::REFL);
         Hit rh;
         if (RV_ABLATE & 8192) rh.hit = false;
-        else rh = trace<STATS, RV_G_REFL ? RV_G_REFL : G, RE>(w, hit.pos, rdir, hround(0.001f), sc);
+        else {
+            constexpr int GG = RV_G_REFL ? RV_G_REFL : G;
+            constexpr bool COLR = RV_COL_REFL && (GG > 1) && RV_DDA_REWALK && GR == 0;   // throughput launches
+            rh = trace<STATS, GG, RE, (RV_DDA_REWALK != 0), false, WV, COLR>(w, hit.pos, rdir, hround(0.001f), sc);
+        }
         if (STATS) { c[CNT_TRACES]++; c[CNT_REFL]++; }
         f3 rc;
         if (rh.hit) {

@@ -365,7 +365,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
     world_set_regions(w, ((uint64_t)w.X * w.Y * w.Z) / 512);
     // 128 B per 512 voxels (bits and CSDF regions), then the sun horizon (rv_device.h horizon_at)
-    c->brick_bytes = horizon_byte(w.coff) + horizon_bytes(w.X, w.Z);
+    c->brick_bytes = dtop_byte(w.coff, w.X, w.Z) + dtop_bytes(w.X, w.Z);
     c->gi_bytes = n_gi(c) * 4;
 
     auto cleanup_fail = [&](rv_status s, const char* what) {
@@ -378,18 +378,22 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (hipMalloc(&c->gi, c->gi_bytes) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "gi");
     hipMemset(c->brick, 0, horizon_byte(w.coff));
     hipMemset(reinterpret_cast<char*>(c->brick) + horizon_byte(w.coff), 0xFF, horizon_bytes(w.X, w.Z));   // no sun exit
+    hipMemset(reinterpret_cast<char*>(c->brick) + dtop_byte(w.coff, w.X, w.Z), 0x7F, dtop_bytes(w.X, w.Z));   // no skip
     hipMemset(c->gi, 0, c->gi_bytes);
     // atlas
     int aw = cfg->atlas_rgba8 ? cfg->atlas_w : 256, ah = cfg->atlas_rgba8 ? cfg->atlas_h : 256;
     if (aw <= 0 || ah <= 0) return cleanup_fail(RV_ERR_INVALID, "atlas dims");
     w.aw = aw; w.ah = ah;
-    if (hipMalloc(&c->atlas, (size_t)aw * ah * 4) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "atlas");
-    if (cfg->atlas_rgba8) {
-        hipMemcpy(c->atlas, cfg->atlas_rgba8, (size_t)aw * ah * 4, hipMemcpyHostToDevice);
-    } else {
-        std::vector<uint32_t> grey((size_t)aw * ah, 0xFF808080u);
-        hipMemcpy(c->atlas, grey.data(), grey.size() * 4, hipMemcpyHostToDevice);
-    }
+    // held in World's tiled layout (rv_device.h atlas_tiled_off): 128-B lines of 2D texel blocks
+    std::vector<uint32_t> tiled(atlas_tiled_texels(aw, ah), 0u);
+    for (int r = 0; r < ah; r++)
+        for (int q = 0; q < aw; q++) {
+            uint32_t t = 0xFF808080u;   // grey without an atlas
+            if (cfg->atlas_rgba8) std::memcpy(&t, static_cast<const uint8_t*>(cfg->atlas_rgba8) + 4 * ((size_t)r * aw + q), 4);
+            tiled[atlas_tiled_off(aw, r, q)] = t;
+        }
+    if (hipMalloc(&c->atlas, tiled.size() * 4) != hipSuccess) return cleanup_fail(RV_ERR_OOM, "atlas");
+    hipMemcpy(c->atlas, tiled.data(), tiled.size() * 4, hipMemcpyHostToDevice);
     c->cfg.atlas_rgba8 = nullptr;
     // frame slot 0 (more with rv_set_frames_in_flight)
     int W = cfg->width, H = cfg->height;
@@ -746,6 +750,8 @@ static rv_status world_top(rv_ctx* c) {
     uint32_t* hz = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->brick) + horizon_byte(c->w.coff));
     const size_t hzb = horizon_bytes(c->w.X, c->w.Z);
     HIP_TRY(c, hipMemsetAsync(hz, 0xFF, hzb, c->stream));   // no sun exit unless built below
+    int* dt = reinterpret_cast<int*>(reinterpret_cast<char*>(c->brick) + dtop_byte(c->w.coff, c->w.X, c->w.Z));
+    HIP_TRY(c, hipMemsetAsync(dt, 0x7F, dtop_bytes(c->w.X, c->w.Z), c->stream));   // no column skip unless built below
     const char* e = getenv("RV_SKY_EXIT");
     if (e && e[0] == '0') return RV_OK;
     if (!c->d_top) HIP_TRY(c, hipMalloc(&c->d_top, 4));
@@ -756,18 +762,22 @@ static rv_status world_top(rv_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(&top, c->d_top, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->w.ytop = std::min((uint32_t)c->w.Y, top + 1u);   // top = max solid y + 1
+    // the column tops: the DDA's empty-column skip (dtop_at; env RV_COL_SKIP=0: off) and the sun horizon's input
+    if (!c->coltop) HIP_TRY(c, hipMalloc(&c->coltop, hzb));
+    HIP_TRY(c, hipMemsetAsync(c->coltop, 0, hzb, c->stream));
+    const char* cs = getenv("RV_COL_SKIP");
+    launch_column_tops(c->stream, c->brick, current_world(c), c->coltop, dt);
+    LAUNCH_CHECK(c);
+    if (cs && cs[0] == '0') HIP_TRY(c, hipMemsetAsync(dt, 0x7F, dtop_bytes(c->w.X, c->w.Z), c->stream));
     // the sun exit of shadow rays (trace_sun): the horizon per brick column for the library's sun
     // (env RV_SUN_EXIT=0: off)
     const char* se = getenv("RV_SUN_EXIT");
     const f3 sun = sun_dir();
     const double hxz = std::sqrt((double)sun.x * sun.x + (double)sun.z * sun.z);
     if ((se && se[0] == '0') || !(sun.y > 0.0f) || hxz == 0.0) return RV_OK;
-    if (!c->coltop) HIP_TRY(c, hipMalloc(&c->coltop, hzb));
-    HIP_TRY(c, hipMemsetAsync(c->coltop, 0, hzb, c->stream));
     // slope shaded 0.1 % low (a lower slope only raises the horizon: conservative)
     const float k = (float)((double)sun.y / hxz * (1.0 - 1e-3));
-    launch_sun_horizon(c->stream, c->brick, current_world(c), c->coltop, hz, (float)(sun.x / hxz),
-                       (float)(sun.z / hxz), k);
+    launch_sun_horizon(c->stream, current_world(c), c->coltop, hz, (float)(sun.x / hxz), (float)(sun.z / hxz), k);
     LAUNCH_CHECK(c);
     return RV_OK;
 }
