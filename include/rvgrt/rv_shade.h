@@ -40,6 +40,9 @@
 #ifndef RV_COL_REFL       // the water reflection's DDA skips the voxel gathers of groups above the terrain
 #define RV_COL_REFL 1     // (rv_device.h trace COL)
 #endif
+#ifndef RV_COL_PRIMARY    // ... the camera rays (render and pre-pass) too (A/B)
+#define RV_COL_PRIMARY 0
+#endif
 #ifndef RV_COL_GI         // ... the GI update's bounce rays too (A/B)
 #define RV_COL_GI 0
 #endif
@@ -60,7 +63,8 @@ __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, 
     f3 dir = ray_dir(f, x, y);
     StepCount sc{};
     RV_GD_KIND(gd::PP_PRIMARY);
-    Hit h = trace<STATS, G, false>(w, f.pos, dir, 0.0f, sc);
+    Hit h = trace<STATS, G, false, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && (G > 1) && RV_DDA_REWALK>(
+        w, f.pos, dir, 0.0f, sc);
     float d = h.hit ? length(sub(h.pos, f.pos)) : 300.0f;
     float s = 1.0f;
     if (STATS) { c[CNT_TRACES]++; c[CNT_PP_PRIMARY]++; c[CNT_UNDEF] += h.undef; }
@@ -157,7 +161,8 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         hit = trace<STATS, G, RE>(wt, f.pos, dir, hround(dist), sc);
     } else
 #endif
-    hit = trace<STATS, G, RE>(w, f.pos, dir, hround(dist), sc);
+    hit = trace<STATS, G, RE, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && GR == 0 && (G > 1) && RV_DDA_REWALK>(
+        w, f.pos, dir, hround(dist), sc);
     if (STATS) { c[CNT_TRACES]++; c[CNT_PRIMARY]++; c[CNT_UNDEF] += hit.undef; }
     f3 color;
     if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER) && (RV_ABLATE & 4)) {
