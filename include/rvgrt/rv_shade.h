@@ -124,7 +124,9 @@ template <uint32_t FEAT> struct TraceCfg {
 };
 
 // computeColor (StateRender.cu:33-146)
-template <bool STATS, uint32_t FEAT, int CB = RV_CONE_GROUP, int GR = 0, class WV = World>
+// COLOK: the launch may take the water reflection's column skip (k_ref_flow: no -- its render waits inside
+// the launch and the skip's registers cost it 3.5 %, profiles/r04/col_skip_atlas_ab.txt)
+template <bool STATS, uint32_t FEAT, int CB = RV_CONE_GROUP, int GR = 0, class WV = World, bool COLOK = true>
 __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, float x, float y,
                                             float dist, float shadow_in, Hit& hit, uint32_t (&c)[NCNT]) {
     const bool prepass = has<FEAT>(f, RV_F_PREPASS);
@@ -178,7 +180,7 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         if (RV_ABLATE & 8192) rh.hit = false;
         else {
             constexpr int GG = RV_G_REFL ? RV_G_REFL : G;
-            constexpr bool COLR = RV_COL_REFL && (GG > 1) && RV_DDA_REWALK && GR == 0;   // throughput launches
+            constexpr bool COLR = RV_COL_REFL && (GG > 1) && RV_DDA_REWALK && GR == 0 && COLOK;   // throughput launches
             rh = trace<STATS, GG, RE, (RV_DDA_REWALK != 0), false, WV, COLR>(w, hit.pos, rdir, hround(0.001f), sc);
         }
         if (STATS) { c[CNT_TRACES]++; c[CNT_REFL]++; }
@@ -274,7 +276,7 @@ __device__ __forceinline__ void clip_pos(const float* P, const float* M, f3 p, f
 
 // renderKernel body for one pixel (StateRender.cu:200-253); returns RGBA8
 template <bool STATS, uint32_t FEAT, bool CAMS = false, bool LATE = false, int CB = RV_CONE_GROUP, int GR = 0,
-          class WV = World>
+          class WV = World, bool COLOK = true>
 __device__ __forceinline__ uint32_t render_pixel(const WV& w, const FrameParams& f, int ix, int iy,
                                                  uint32_t (&c)[NCNT], const HalfWin* hwin = nullptr) {
     float x = (float)ix / (float)f.W, y = (float)iy / (float)f.H;
@@ -284,7 +286,7 @@ __device__ __forceinline__ uint32_t render_pixel(const WV& w, const FrameParams&
         shadow = bilinear_tex(f, x, y, hwin);
     }
     Hit h;
-    f3 col = compute_color<STATS, FEAT, CB, GR, WV>(w, f, x, y, dist, shadow, h, c);
+    f3 col = compute_color<STATS, FEAT, CB, GR, WV, COLOK>(w, f, x, y, dist, shadow, h, c);
     float mvx = 0.0f, mvy = 0.0f, dep = 1.0f;
     if (h.hit) {   // mat_mul_vec (cumath.cuh:47-54), glm column-major
         float pc[4], cc[4];

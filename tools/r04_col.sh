@@ -11,7 +11,7 @@ fi
 for rep in 1 2; do
 for line in ${LINES:-c4_P1 c4_P0 c3_P1 c5_P1}; do c=${line%_*}; pose=${line#*_}
 for v in ${VARIANTS:-main nocol colgi halfwin}; do lib=""; [ "$v" != main ] && lib=$PWD/rvgrt_amd/variants/$v/librvgrt_hip.so
-  RVGRT_LIB=$lib timeout -k 10 200 python bench.py --config $c --pose $pose --steps 200 --cpu-seconds 0 > gpurun_out/col_b.json 2>/dev/null || exit 3
+  RVGRT_LIB=$lib timeout -k 10 200 python bench.py --config $c --pose $pose --loop ${LOOP:-native} --steps 200 --cpu-seconds 0 > gpurun_out/col_b.json 2>/dev/null || exit 3
   python3 -c "
 import json; d=[json.loads(l) for l in open('gpurun_out/col_b.json') if l.startswith('{')][-1]; print('$line $v', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
 done; done; done
