@@ -216,17 +216,20 @@ def test_reference_native_config_draw_cuda(rv, atlas, oracle):
     r.close()
 
 
-@pytest.mark.parametrize("cfgname,grp", [("c3", 0), ("c4", 0), ("c3", 8), ("c4", 8)])
-def test_fullsize_pipelined_frames(rv, atlas, cfgname, grp):
+@pytest.mark.parametrize("cfgname,grp,pose", [("c3", 0, "P0"), ("c4", 0, "P0"), ("c3", 8, "P0"), ("c4", 8, "P0"),
+                                              ("c4", 0, "P1"), ("c3", 8, "P1")])
+def test_fullsize_pipelined_frames(rv, atlas, cfgname, grp, pose):
     """The C3/C4 frame loop as bench.py runs it (pipelined launches: render
     k | GI update k+1 | pre-pass k+1; or grouped: 8 frames per launch) against UpdateGIData + drawCUDA one
     frame at a time (drawCUDA's two launches, rv_set_flow(0)) on the same full-size world: colour, depth
     and the GI grid bit-identical after 6 frames (the one-at-a-time frames are checked against the oracle
-    by the tests above)."""
+    by the tests above).  P1 (water-heavy): the water reflection's empty-column skip of the pipelined and
+    grouped launches (rv_device.h trace COL) on most of the frame; the one-at-a-time frames' two launches
+    equal the flow launch, which does not take the skip, and the oracle (test_fullsize_drop_in_flow_frames)."""
     from rvgrt_amd.configs import CONFIGS, pose_f32
     cfg = CONFIGS[cfgname]
     W, H = cfg.width, cfg.height
-    cam, vp = rv.camera_from_pose(*pose_f32(cfg), W, H)
+    cam, vp = rv.camera_from_pose(*pose_f32(cfg, pose), W, H)
     rs = []
     for pipe in (1, 0):
         r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=atlas)
