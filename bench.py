@@ -10,7 +10,10 @@ reflection shadow, 6-cone voxel GI) over a GI grid after 2 full sweeps, with
 the reference's per-frame GI update (UpdateGIData, 262144 cells) before every
 frame.  W untimed frames, then K timed frames bracketed by a barrier +
 device synchronize on both sides; the time is the max over ranks.  Rank 0
-prints ONE JSON line.
+prints ONE JSON line.  Before the W warm-up frames, --settle (default 100)
+tops the untimed frames of the same loop up to that many (reported as
+"settle_frames"): the GPU's clocks and caches need tens of ms after the
+set-up's idle gaps, far more than a handful of 0.4-ms frames.
 
 Multi-GPU: the frame is split into interleaved screen tiles (rv_set_tile_shard),
 every rank renders its tiles of the same frame against its own locally
@@ -95,6 +98,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle", type=int, default=100,
+                    help="untimed frames of the same loop before the --warmup frames bring the total untimed "
+                         "frames to at least this many (0: off): a 4K frame is ~0.4 ms, and the GPU's clocks and "
+                         "caches take tens of ms to settle after the set-up's idle gaps (20 timed frames after 5 "
+                         "warm-up frames read 0.444 ms/frame, after 100 0.429, 200 after 20 0.425; "
+                         "profiles/r04/settle.txt)")
     ap.add_argument("--config", default="c4",
                     help="c1..c5 (default c4: 1024^3, 3840x2160, the reference frame with 2-bounce GI and a GI "
                          "update every frame -- the north star's 1-GPU workload, BASELINE configs[3])")
@@ -243,7 +252,9 @@ def main():
     n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if nfl > 1 else min(args.steps, 10)
     if group >= 2:   # whole groups: the timing pass records only full-group launches
         n_stage_frames = group * max(3, min(args.steps // group, 6))
-    n_path = args.warmup + args.steps + n_stage_frames + 9 + 2 + 5 * max(group, 0)   # + the group-latency calls
+    settle = max(0, args.settle - args.warmup)   # untimed frames before the warm-up (--settle)
+    w0 = settle + args.warmup                     # the first timed frame of the path
+    n_path = w0 + args.steps + n_stage_frames + 9 + 2 + 5 * max(group, 0)   # + the group-latency calls
     pan = args.pan if args.camera == "path" else 0.0
     path = camera_path((pos, yaw, pitch), W, H, n_path, pan=pan, ref_compat=args.camera == "path")
     if args.camera == "static":   # the round-1 bench: one camera, time 0, no jitter
@@ -259,7 +270,7 @@ def main():
     # ---------------------------------------------------------------- work census
     # Frames with counters on: rays per frame and algorithmic bytes, the mean
     # over 8 frames spread over the timed part of the path.
-    census = np.linspace(args.warmup, args.warmup + max(args.steps - 1, 0), 8).astype(int)
+    census = np.linspace(w0, w0 + max(args.steps - 1, 0), 8).astype(int)
     r.stats_reset()
     for i in census:
         d = path[i]
@@ -417,9 +428,11 @@ def main():
             finish()
 
     if native:
+        if settle:
+            run_native(settle)
         run_native(args.warmup)
     else:
-        for _ in range(args.warmup):
+        for _ in range(settle + args.warmup):
             step()
         drain()
     torch.cuda.synchronize(dev)
@@ -594,7 +607,7 @@ def main():
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and world_size == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(r, cfg, path[args.warmup], flags, atlas, args.cpu_seconds)
+        cpu = cpu_baseline(r, cfg, path[w0], flags, atlas, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -605,6 +618,7 @@ def main():
             "n_gpus": world_size,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_frames": settle,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(fps, 2),
             "latency_ms": latency_ms,
