@@ -11,9 +11,11 @@ the reference's per-frame GI update (UpdateGIData, 262144 cells) before every
 frame.  W untimed frames, then K timed frames bracketed by a barrier +
 device synchronize on both sides; the time is the max over ranks.  Rank 0
 prints ONE JSON line.  Before the W warm-up frames, --settle (default 100)
-tops the untimed frames of the same loop up to that many (reported as
-"settle_frames"): the GPU's clocks and caches need tens of ms after the
-set-up's idle gaps, far more than a handful of 0.4-ms frames.
+tops the untimed frames up to that many (reported as "settle_frames"): the
+first frames of the camera path, rendered by the same loop, after which the
+path starts again, so the warm-up and timed frames -- the views measured --
+are the same as without it.  The GPU's clocks and caches need tens of ms
+after the set-up's idle gaps, far more than a handful of 0.4-ms frames.
 
 Multi-GPU: the frame is split into interleaved screen tiles (rv_set_tile_shard),
 every rank renders its tiles of the same frame against its own locally
@@ -252,9 +254,11 @@ def main():
     n_stage_frames = nfl * max(1, min(args.steps // nfl, 10)) if nfl > 1 else min(args.steps, 10)
     if group >= 2:   # whole groups: the timing pass records only full-group launches
         n_stage_frames = group * max(3, min(args.steps // group, 6))
-    settle = max(0, args.settle - args.warmup)   # untimed frames before the warm-up (--settle)
-    w0 = settle + args.warmup                     # the first timed frame of the path
-    n_path = w0 + args.steps + n_stage_frames + 9 + 2 + 5 * max(group, 0)   # + the group-latency calls
+    # --settle: untimed frames before the warm-up, taken from the start of the camera path, which then
+    # starts again -- the warm-up and timed frames are the same frames (the same views) with or without it
+    settle = max(0, args.settle - args.warmup)
+    w0 = args.warmup                              # the first timed frame of the path
+    n_path = max(w0 + args.steps + n_stage_frames + 9 + 2 + 5 * max(group, 0), settle + 1)   # + the group-latency calls
     pan = args.pan if args.camera == "path" else 0.0
     path = camera_path((pos, yaw, pitch), W, H, n_path, pan=pan, ref_compat=args.camera == "path")
     if args.camera == "static":   # the round-1 bench: one camera, time 0, no jitter
@@ -427,12 +431,18 @@ def main():
         while pending:
             finish()
 
-    if native:
-        if settle:
+    if settle:
+        if native:
             run_native(settle)
+        else:
+            for _ in range(settle):
+                step()
+            drain()
+        cursor[0] = 0        # the warm-up and timed frames start the path again
+    if native:
         run_native(args.warmup)
     else:
-        for _ in range(settle + args.warmup):
+        for _ in range(args.warmup):
             step()
         drain()
     torch.cuda.synchronize(dev)
