@@ -8,7 +8,7 @@ if [ "${TESTS:-1}" = 1 ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/col_tests.log 2>&1
   rc=$?; tail -3 gpurun_out/col_tests.log; [ $rc = 0 ] || exit 3
 fi
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
 for line in ${LINES:-c4_P1 c4_P0 c3_P1 c5_P1}; do c=${line%_*}; pose=${line#*_}
 for v in ${VARIANTS:-main nocol colgi halfwin}; do lib=""; [ "$v" != main ] && lib=$PWD/rvgrt_amd/variants/$v/librvgrt_hip.so
   RVGRT_LIB=$lib timeout -k 10 200 python bench.py --config $c --pose $pose --loop ${LOOP:-native} --steps 200 --cpu-seconds 0 > gpurun_out/col_b.json 2>/dev/null || exit 3
