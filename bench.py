@@ -16,6 +16,16 @@ first frames of the camera path, rendered by the same loop, after which the
 path starts again, so the warm-up and timed frames -- the views measured --
 are the same as without it.  The GPU's clocks and caches need tens of ms
 after the set-up's idle gaps, far more than a handful of 0.4-ms frames.
+Only the camera restarts: the settle frames run the per-frame GI update too
+(UpdateGIData before every drawCUDA, src/main.cpp:119-132), so the GI grid and
+its rolling window are those of a run that has rendered the settle frames
+already -- as in any longer run of the reference's loop, whose grid never
+stops updating.
+
+Drop-in leg (one GPU, C3-C5, --dropin-leg 1): after the timed region the same
+context renders --steps more frames through renderLoop's own calls
+(rv_update_gi_data, then rv_draw_cuda of that frame's camera; no camera
+look-ahead), timed the same way, reported as "dropin" with its own roofline.
 
 Multi-GPU: the frame is split into interleaved screen tiles (rv_set_tile_shard),
 every rank renders its tiles of the same frame against its own locally
@@ -160,6 +170,11 @@ def main():
                          "two launches with the GI update on the side stream)")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
+    ap.add_argument("--dropin-leg", type=int, default=1,
+                    help="one GPU, native loop, reference frames (C3-C5): after the timed region, time the same "
+                         "number of frames through renderLoop's own calls (rv_update_gi_data, then rv_draw_cuda, "
+                         "one frame per call, no knowledge of the next camera: src/main.cpp:119-132) and report "
+                         "them as \"dropin\" (ms/frame, cold latency, that loop's roofline); 0 = off")
     args = ap.parse_args()
 
     import torch
@@ -614,6 +629,16 @@ def main():
                 "gathers_per_launch": int(gathers), "gather_rate": round(gather_rate / 1e9, 2),
                 "gather_unit": "G lane-gathers/s"}
 
+    # ---------------------------------------------------------------- drop-in leg
+    # renderLoop's own calls (src/main.cpp:119-132): UpdateGIData, then drawCUDA of the frame's camera, one
+    # frame per call -- what a caller of the drop-in boundary gets (the native loop above hands over the next
+    # frame's camera).  Same context, world and camera path; warm-up + timed frames, a timing pass for the
+    # k_ref_flow launch's roofline and the cold latency of one renderLoop frame.
+    dropin = None
+    if (args.dropin_leg and native and world_size == 1 and not drawcuda and gi_per_frame and prepass
+            and args.path == "fused" and args.flow):
+        dropin = dropin_leg(r, stream, cfg, flags, pos, yaw, pitch, pan, args, gi_stats, traffic_dir=ROOT)
+
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and world_size == 1 and args.cpu_seconds > 0:
@@ -666,6 +691,7 @@ def main():
             "root_weight": float(os.environ.get("RV_SHARD_ROOT_WEIGHT", "1")) if world_size > 1 and native else None,
             "gather_check": gather_check,
             "roofline": roofline,
+            "dropin": dropin,
             "cpu_baseline": cpu,
             "world_build_s": round(world_s, 3),
             "stats": st_all,
@@ -676,6 +702,98 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def dropin_leg(r, stream, cfg, flags, pos, yaw, pitch, pan, args, gi_stats, traffic_dir):
+    """The drop-in leg: --warmup + --steps frames of renderLoop's calls (rv_update_gi_data, then
+    rv_draw_cuda with ref_compat, one frame per call) on the bench's context, timed between two device
+    synchronizes; then a timing pass of 10 frames (HIP events around each k_ref_flow launch on its stream)
+    and the median cold latency of 9 renderLoop frames.  The roofline's algorithmic bytes are the flow
+    launch's: the frame's render + pre-pass (census frames with the reference's minDist fetch, as
+    rv_draw_cuda renders) + the GI window it computes ahead (the bench's GI census)."""
+    import torch
+    import rvgrt_amd as rv
+    from rvgrt_amd.configs import camera_path
+
+    W, H = cfg.width, cfg.height
+    n = args.warmup + args.steps + 10 + 9
+    path = camera_path((pos, yaw, pitch), W, H, n, pan=pan, ref_compat=True)
+    dflags = flags | rv.RV_F_REF_FETCH
+    r.set_stream(stream.cuda_stream)
+    census = np.linspace(args.warmup, args.warmup + max(args.steps - 1, 0), 8).astype(int)
+    r.stats_reset()
+    for i in census:
+        d = path[i]
+        r.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time,
+                jx=d.jitter_x, jy=d.jitter_y, flags=dflags | rv.RV_F_STATS)
+    st = {name: {k: v / len(census) for k, v in r.stats(i).items()} for i, name in enumerate(rv._lib.STAGES)}
+    rays = int(round(sum(v["traces"] for k, v in st.items() if k != "gi")))
+    b = algorithmic_bytes(st["primary"], W * H, (W // 2) * (H // 2), True, "fused_render")
+    b += algorithmic_bytes(st["pp_primary"], W * H, (W // 2) * (H // 2), True, "fused_prepass")
+    if gi_stats is not None:
+        b += (4 * gi_stats["dda_steps"] + gi_stats["sphere_steps"] + gi_stats["csdf_checks"]
+              + 20 * gi_stats["tex_samples"] + 8 * min(262144, (cfg.n // 4) ** 3))
+    cur = [0]
+
+    def frame():
+        d = path[cur[0]]
+        cur[0] += 1
+        r.update_gi_data()
+        c = d.cam
+        r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(d.vp),
+                    np.ctypeslib.as_array(d.prev_vp), jitter_x=0.0, jitter_y=d.time)
+
+    _, fb0 = r.flow_info()[1:]
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    r.timing_enable(22)
+    for _ in range(10):
+        frame()
+    torch.cuda.synchronize()
+    per_stage_ms, _ = r.timing_stages()
+    launches = r.timing_launches()
+    r.timing_enable(0)
+    lat = []
+    for _ in range(9):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        frame()
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t1) * 1000.0)
+    active, nflow, fb = r.flow_info()
+    launch_ms = per_stage_ms["primary"] / launches["primary"] if launches["primary"] else 0.0
+    achieved = b / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    traffic, limit = None, None
+    tpath = os.path.join(traffic_dir, "profiles", f"traffic_{cfg.name}" + ("" if args.pose == "P0" else f"_{args.pose}")
+                         + "_drawcuda.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            tj["_path"] = tpath
+            if tj.get("kernel", "").startswith("k_ref_flow"):
+                traffic = tj.get("hbm_bytes_per_launch")
+                limit = binding_limit(tj, launch_ms)
+        except Exception:
+            traffic = None
+    ms = elapsed * 1000.0 / args.steps
+    return {"loop": "renderLoop calls: rv_update_gi_data + rv_draw_cuda (ref_compat), one frame per call",
+            "ms_per_step": round(ms, 4), "fps": round(1000.0 / ms, 2), "steps": args.steps, "warmup": args.warmup,
+            "mrays_per_s": round(rays * 1000.0 / ms / 1e6, 2), "rays_per_frame": rays,
+            "latency_ms": round(float(np.median(lat)), 4),
+            "latency_mode": "cold renderLoop frame: UpdateGIData + drawCUDA of one frame from an idle device",
+            "flow_active": bool(active), "flow_fallbacks": fb - fb0,
+            "roofline": {"bound": "hbm", "limit": limit, "kernel": "k_ref_flow", "achieved": round(achieved, 2),
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": int(b),
+                         "avg_launch_ms": round(launch_ms, 4), "frames_per_launch": 1,
+                         "traffic_frac": (round(traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+                                          if traffic and launch_ms > 0 else None)}}
 
 
 def cpu_baseline(r, cfg, d, flags, atlas, budget_s):

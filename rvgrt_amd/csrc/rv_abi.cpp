@@ -174,6 +174,7 @@ struct rv_ctx {
     unsigned long long* flow_half = nullptr; size_t flow_tiles = 0;
     uint32_t flow_epoch = 0;
     unsigned long long* flow_fb = nullptr;
+    hipEvent_t ev_flow = nullptr;   // recorded after every flow launch, on the stream it ran on
     uint64_t flow_launches = 0;
     // env RV_GI_PAIRS: latency-variant launches trace a GI cell's two rays on a lane pair (1 all, 0 none);
     // default -1: a rank's tile share only -- its GI part is 1/N of the cells and its longest GI waves
@@ -530,6 +531,7 @@ void rv_destroy(rv_ctx* c) {
     if (c->ev_world) hipEventDestroy(c->ev_world);
     hipFree(c->flow_half); hipFree(c->flow_fb);
     if (c->ev_spec) hipEventDestroy(c->ev_spec);
+    if (c->ev_flow) hipEventDestroy(c->ev_flow);
     hipFree(c->cam_dev);
     if (c->cam_host) hipHostFree(c->cam_host);
     if (c->cam_ev) hipEventDestroy(c->cam_ev);
@@ -672,12 +674,15 @@ rv_status rv_set_flow(rv_ctx* c, int32_t on) {
 
 rv_status rv_flow_info(rv_ctx* c, int32_t* active, uint64_t* launches, uint64_t* fallbacks) {
     if (!c) return RV_ERR_INVALID;
-    if (active) *active = c->flow;
+    // in effect: on, one frame slot, the megakernel path (flow_eligible's frame-independent part)
+    if (active) *active = c->flow && c->megakernel && c->slots.size() == 1;
     if (launches) *launches = c->flow_launches;
     if (fallbacks) {
         *fallbacks = 0;
         if (c->flow_fb) {
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            // the last flow launch may have run on another stream than the current one (rv_set_stream
+            // between frames): wait for the event recorded after it
+            if (c->ev_flow) HIP_TRY(c, hipEventSynchronize(c->ev_flow));
             unsigned long long v = 0;
             HIP_TRY(c, hipMemcpy(&v, c->flow_fb, 8, hipMemcpyDeviceToHost));
             *fallbacks = v;
@@ -1186,8 +1191,13 @@ static rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles, int which = 3)
 // The GI part runs only while the caller updates the grid before every frame (renderLoop's
 // UpdateGIData -> drawCUDA, src/main.cpp:119-132): its window is the one rv_update_gi_data will
 // apply next, read from the grid this frame renders with; that call then only copies it back.
+// The render part reads its 8 half-res taps per pixel from an 8x8-texel LDS window (rv_frame.h HalfWin) that
+// holds every tap only when the half-res images are W/2 x H/2 (Appendix R6); a tap outside it would read the
+// global image, which the same launch's pre-pass writes without ordering -- so the flow launch requires that
+// shape (make_params always sets it; the check keeps any other resolution on the two-launch path).
 static bool flow_eligible(const rv_ctx* c, const FrameParams& f) {
-    return c->flow && c->megakernel && c->slots.size() == 1 && (f.flags & RV_F_PREPASS) != 0 && f.hw > 0 && f.hh > 0;
+    return c->flow && c->megakernel && c->slots.size() == 1 && (f.flags & RV_F_PREPASS) != 0 && f.hw > 0 && f.hh > 0 &&
+           f.hw == f.W / 2 && f.hh == f.H / 2;
 }
 
 static rv_status flow_frame(rv_ctx* c, FrameParams f) {
@@ -1246,6 +1256,8 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     launch_ref_flow(c->stream, current_world(c), f, p);
     LAUNCH_CHECK(c);
     c->flow_launches++;
+    if (!c->ev_flow) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_flow, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(c->ev_flow, c->stream));
     if (timed) {
         c->ev_stage[e0 + 1] = -1;
         HIP_TRY(c, hipEventRecord(c->ev[e0 + 1], c->stream));

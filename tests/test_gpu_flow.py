@@ -164,3 +164,29 @@ def test_flow_stats_frame_counts(rv, atlas):
         r.close()
     for k in (0, 2):
         assert out[0][k] == out[1][k], k
+
+
+def test_flow_fallback_throughput_variant_4k(rv, atlas, monkeypatch):
+    """The forced fallback on a 3840x2160 frame: 129,600 render waves, so the
+    flow launch is the throughput instantiation (render look-ahead RV_G_REF, the
+    variant C4/C5 frames run) -- its fallback (prepass_eval at that look-ahead)
+    must give the two-launch frame's texels too, and every render wave counts."""
+    from rvgrt_amd.configs import CONFIGS, camera_path, pose_f32
+    lg, W, H, rays = 8, 3840, 2160, 5000
+    seq = camera_path(pose_f32(CONFIGS["c1"], "P0"), W, H, 3, pan=0.01, ref_compat=True)
+    b = _make(rv, atlas, lg, W, H, rays, 0)
+    monkeypatch.setenv("RV_FLOW_FORCE_FALLBACK", "1")
+    monkeypatch.setenv("RV_FLOW_SPIN", "2")
+    a = _make(rv, atlas, lg, W, H, rays, 1)
+    for k in range(2):
+        for r in (a, b):
+            r.update_gi_data()
+            _draw(r, seq[k])
+        for x, y in zip(_images(a, rv), _images(b, rv)):
+            assert np.array_equal(x, y), k
+    assert np.array_equal(a.world_export(rv.RV_WORLD_GI), b.world_export(rv.RV_WORLD_GI))
+    waves = (W // 8) * (H // 8)
+    assert waves > 49152
+    assert a.flow_info() == (True, 2, 2 * waves)
+    a.close()
+    b.close()

@@ -9,6 +9,10 @@ whole frame.  Above it, where an oracle world build is too slow for a test,
 the GPU world is exported and checked with what the oracle answers at any
 size:
 
+* the whole world first: bits, CSDF and the GI grid the config renders with
+  hash equal to the oracle's own whole-grid build (tests/world_golden.py,
+  tests/test_gpu_full_world.py), so the oracle never renders on a world it
+  did not compute itself;
 * voxel bits: 200k sampled voxels against the oracle's Evaluate (> 0.7);
 * CSDF: zero exactly where a coarse 2x2x2 cell holds a solid voxel, over the
   whole grid (catches any addressing error of the brick layout);
@@ -25,6 +29,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
+import world_golden as WG
 from conftest import random_rays
 
 pytestmark = pytest.mark.gpu
@@ -49,9 +54,11 @@ def coarse_solid(bits, dims, z0, z1):
     return b.reshape(v.shape[0], Y // 2, X // 2).astype(bool)
 
 
-def check_world_rays_gi(r, rv, oracle, atlas, log2, seed, gi_window=True):
+def check_world_rays_gi(r, rv, oracle, atlas, log2, seed, golden, gi_window=True, stage=None):
     """The exported GPU world against the oracle's answers; returns the oracle
-    world holding it."""
+    world holding it.  golden: the config (or world fixture) whose whole-grid
+    oracle hashes the world must match first."""
+    WG.assert_world(r, rv, golden, stage=stage)
     lx, ly, lz = log2
     X, Y, Z = 1 << lx, 1 << ly, 1 << lz
     ow = oracle.OracleWorld(lx, ly, lz, atlas=atlas)
@@ -167,7 +174,7 @@ def test_fullsize_world_traversal_gi_frame_rows(rv, atlas, oracle, cfgname, pose
     for s in range(max(cfg.gi_sweeps, 0)):
         r.gi_update(s)
     r.sync()
-    ow = check_world_rays_gi(r, rv, oracle, atlas, (lg,) * 3, lg, gi_window=cfg.gi_sweeps >= 0)
+    ow = check_world_rays_gi(r, rv, oracle, atlas, (lg,) * 3, lg, cfgname, gi_window=cfg.gi_sweeps >= 0)
     cam, vp = rv.camera_from_pose(*pose_f32(cfg, pose), W, H)
     r.frame(cam, vp)
     # the whole frame: every pixel's RGBA8, MV and depth
@@ -190,7 +197,7 @@ def test_reference_native_config_draw_cuda(rv, atlas, oracle):
     r.world_build()
     r.update_gi_data()              # frame 0: cells [0, 262144)
     r.sync()
-    ow = check_world_rays_gi(r, rv, oracle, atlas, log2, 12)
+    ow = check_world_rays_gi(r, rv, oracle, atlas, log2, 12, "native", stage="gi_window0")
     f32 = lambda v: float(np.float32(v))
     cam, vp = rv.camera_from_pose((128.0, 350.0, 128.0), f32(-0.7), f32(-math.pi - 0.3), W, H)
     d = rv.camera_dict(cam, vp)
@@ -276,6 +283,12 @@ def test_fullsize_drop_in_flow_frames(rv, atlas, oracle, cfgname, pose):
             r.gi_update(s)
         r.set_flow(flow)
         rs.append(r)
+    WG.assert_world(rs[0], rv, cfgname)   # bits, CSDF and the swept GI grid: the oracle's own whole builds
+    lg = cfg.log2_n
+    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas)
+    ow.bits[:] = rs[0].world_export(rv.RV_WORLD_BITS)
+    ow.csdf[:] = rs[0].world_export(rv.RV_WORLD_CSDF)
+    ow.gi[:] = rs[0].world_export(rv.RV_WORLD_GI)
     kinds = (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH, rv.RV_IMAGE_HALF_DIST, rv.RV_IMAGE_HALF_SHADOW)
     for k in range(5):
         d = seq[k]
@@ -288,11 +301,11 @@ def test_fullsize_drop_in_flow_frames(rv, atlas, oracle, cfgname, pose):
             assert np.array_equal(rs[0].readback(kind), rs[1].readback(kind)), (k, kind)
         assert np.array_equal(rs[0].world_export(rv.RV_WORLD_GI), rs[1].world_export(rv.RV_WORLD_GI)), k
     assert rs[0].flow_info()[1:] == (5, 0)
-    lg = cfg.log2_n
-    ow = oracle.OracleWorld(lg, lg, lg, atlas=atlas)
-    ow.bits[:] = rs[0].world_export(rv.RV_WORLD_BITS)
-    ow.csdf[:] = rs[0].world_export(rv.RV_WORLD_CSDF)
-    ow.gi[:] = rs[0].world_export(rv.RV_WORLD_GI)
+    # the 5 UpdateGIData windows (frames 0-4, rolling offset from 0; src/CoarseArray.cu:376-395) by the
+    # oracle on its own swept grid: the grid the last frame renders with
+    for fno in range(5):
+        ow.gi_update(fno, first=fno * WG.RAYPS, count=WG.RAYPS)
+    assert np.array_equal(rs[0].world_export(rv.RV_WORLD_GI), ow.gi)
     d = seq[4]
     check_rows(rs[0], rv, oracle, ow, W, H, cfg.flags | rv.RV_F_REF_FETCH,
                rv.camera_dict(d.cam, np.ctypeslib.as_array(d.vp)), None, time=d.time, nrows=None,
