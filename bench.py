@@ -242,7 +242,7 @@ def main():
         raise SystemExit("--loop drawcuda is the one-GPU drop-in loop")
     # Grouped reference frames (rv_set_frame_group) when a rank's render part is latency-bound (<= 48 K
     # waves of 64 pixels, as the latency-mode pipelined variant): the group's frames share one tail.
-    # tools/shard_probe.py / tools/r03_ab.sh (profiles/r03/), 64-px tiles: C3 on one GPU 0.2234 -> 0.2063 ms
+    # tools/shard_probe.py (profiles/r03/), 64-px tiles: C3 on one GPU 0.2234 -> 0.2063 ms
     # at 8 frames per launch (0.2089 at 16); the slowest C4 rank share at 8 ranks 163.5 -> 93.2 -> 87.7 us/frame
     # at 8 / 16, C5 198.1 -> 122.0 -> 114.1, at 4 ranks C4 182.4 -> 162.0 at 16.  Throughput-bound launches
     # keep the per-frame pipeline: C4 one GPU 0.491 -> 0.553 ms at 16, a 2-rank C4 share 278.9 -> 307.5 us.

@@ -31,9 +31,13 @@ void build(HostWorld& h, int lx, int ly, int lz, const uint32_t* bits, const uin
     w.fX = (float)w.X; w.fY = (float)w.Y; w.fZ = (float)w.Z;
     const uint64_t nbricks = ((uint64_t)w.X * w.Y * w.Z) / 512;
     world_set_regions(w, nbricks);
-    // 128 B per brick, then the sun horizon (UINT32_MAX: no sun exit until world_horizon builds it)
-    h.brick.assign((size_t)(((uint64_t)w.X * w.Y * w.Z) / 16) + horizon_bytes(w.X, w.Z) / 4, 0u);
-    std::fill(h.brick.begin() + (long)(horizon_byte(w.coff) / 4), h.brick.end(), 0xFFFFFFFFu);
+    // 128 B per brick, then the sun horizon (UINT32_MAX: no sun exit until world_horizon builds it), then
+    // the DDA's column-neighbourhood tops (0x7F7F7F7F: no column skip until world_dtop builds them)
+    h.brick.assign((size_t)(((uint64_t)w.X * w.Y * w.Z) / 16) + horizon_bytes(w.X, w.Z) / 4 + dtop_bytes(w.X, w.Z) / 4,
+                   0u);
+    std::fill(h.brick.begin() + (long)(horizon_byte(w.coff) / 4),
+              h.brick.begin() + (long)(dtop_byte(w.coff, w.X, w.Z) / 4), 0xFFFFFFFFu);
+    std::fill(h.brick.begin() + (long)(dtop_byte(w.coff, w.X, w.Z) / 4), h.brick.end(), 0x7F7F7F7Fu);
     for (uint64_t z = 0; z < (uint64_t)w.Z; z++)
         for (uint64_t y = 0; y < (uint64_t)w.Y; y++)
             for (uint64_t x = 0; x < (uint64_t)w.X; x++) {
@@ -92,6 +96,35 @@ void world_horizon(HostWorld& h, const float* sun, std::vector<uint32_t>& coltop
             hz[(uint32_t)i | ((uint32_t)j << lcx)] = horizon_column(coltop.data(), ncx, ncz, lcx, i, j, (float)(sun[0] / hxz),
                                                                     (float)(sun[2] / hxz), k, (float)w.ytop);
     std::copy(hz.begin(), hz.end(), h.brick.begin() + (long)(horizon_byte(w.coff) / 4));   // where horizon_at reads
+}
+
+// The DDA's empty-column skip table (dtop_at) as rv_abi.cpp's world_top builds it: the 2x2-column tops
+// (k_column_top: brick_subcolumn_tops), then per brick column the highest of them over the 3x3 brick
+// columns around it (k_dtop).
+void world_dtop(HostWorld& h) {
+    World& w = h.w;
+    const int ncx = w.X >> 1, ncz = w.Z >> 1, lcx = w.lbx + 2, nbx = w.X >> 3, nbz = w.Z >> 3;
+    std::vector<uint32_t> coltop((size_t)ncx * ncz, 0u);
+    const uint64_t nb = ((uint64_t)w.X * w.Y * w.Z) / 512;
+    for (uint64_t b = 0; b < nb; b++) {
+        uint32_t bx, by, bz;
+        brick_coords(w, b, bx, by, bz);
+        uint32_t t[16];
+        brick_subcolumn_tops(&h.brick[bits_word_index(b, 0)], by, t);
+        for (uint32_t q = 0; q < 16; q++) {
+            uint32_t& c = coltop[(bx * 4u + (q & 3u)) | ((bz * 4u + (q >> 2)) << (uint32_t)lcx)];
+            c = t[q] > c ? t[q] : c;
+        }
+    }
+    int* dt = reinterpret_cast<int*>(reinterpret_cast<char*>(h.brick.data()) + dtop_byte(w.coff, w.X, w.Z));
+    for (int bz = 0; bz < nbz; bz++)
+        for (int bx = 0; bx < nbx; bx++) {
+            uint32_t t = 0;
+            for (int z = std::max(bz - 1, 0) * 4; z < std::min(bz + 2, nbz) * 4; z++)
+                for (int x = std::max(bx - 1, 0) * 4; x < std::min(bx + 2, nbx) * 4; x++)
+                    t = std::max(t, coltop[(uint32_t)x | ((uint32_t)z << lcx)]);
+            dt[bx | (bz << w.lbx)] = (int)t;
+        }
 }
 
 template <int G, bool REUSE, bool RW = true>
@@ -175,6 +208,34 @@ int rvh_trace_sun(int g8, int lx, int ly, int lz, const uint32_t* bits, const ui
         q.normal[0] = r.normal.x; q.normal[1] = r.normal.y; q.normal[2] = r.normal.z;
         q.u = r.u; q.v = r.v; q.hit = r.hit; q.undef = r.undef;
         q.sphere = (int)sc.sphere; q.dda = (int)sc.dda; q.check = (int)sc.check; q.pad = 0;
+    }
+    return 0;
+}
+
+// The empty-column skip (trace COL = true, look-ahead 4 or 8 with re-walk, the sky exit and the dtop table
+// built as the library builds it): the variant the water reflections of the pipelined and grouped launches
+// take.  col = 0 traces the same rays without the skip (same sky exit), for comparison.
+int rvh_trace_col(int g8, int col, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* org,
+                  const float* dir, const float* dist, int64_t n, HostHit* out) {
+    HostWorld h;
+    build(h, lx, ly, lz, bits, csdf);
+    h.w.ytop = world_ytop(h);
+    world_dtop(h);
+    for (int64_t i = 0; i < n; i++) {
+        StepCount sc{};
+        const f3 o = V(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
+        const f3 d = V(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+        const float t = hround(dist[i]);
+        Hit r;
+        if (g8) r = col ? trace<true, 8, false, true, false, World, true>(h.w, o, d, t, sc)
+                        : trace<true, 8, false, true, false, World, false>(h.w, o, d, t, sc);
+        else r = col ? trace<true, 4, false, true, false, World, true>(h.w, o, d, t, sc)
+                     : trace<true, 4, false, true, false, World, false>(h.w, o, d, t, sc);
+        HostHit& q = out[i];
+        q.pos[0] = r.pos.x; q.pos[1] = r.pos.y; q.pos[2] = r.pos.z;
+        q.normal[0] = r.normal.x; q.normal[1] = r.normal.y; q.normal[2] = r.normal.z;
+        q.u = r.u; q.v = r.v; q.hit = r.hit; q.undef = r.undef;
+        q.sphere = (int)sc.sphere; q.dda = (int)sc.dda; q.check = (int)sc.check; q.pad = (int)sc.col_skip;
     }
     return 0;
 }

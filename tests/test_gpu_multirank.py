@@ -194,3 +194,65 @@ def test_loopback_missing_rank_times_out(rv, atlas):
     comm.close()
     r.close()
     group.close()
+
+
+@pytest.mark.parametrize("cfgname,N,w0,grp", [("c4", 4, 0.94, 0), ("c4", 4, 0.94, 16), ("c5", 8, 0.87, 16)])
+def test_loopback_ranks_full_size(rv, atlas, monkeypatch, cfgname, N, w0, grp):
+    """The N-rank loop at BASELINE's full sizes: C4 (1024^3, 3840x2160, 2 GI sweeps)
+    on 4 ranks and C5 (2048^3) on 8, 64-px tiles dealt by weight, RGB24 packing, per-frame pipelined
+    (group 0: the sharded GI update's all-gather every frame) or grouped (16 frames per launch: sharded
+    phase A, one record all-gather per group).  20 frames in two calls -- a whole group and a partial
+    one, the second call starting from the kept work -- and rank 0's assembled frame and every rank's GI
+    grid equal to one context rendering UpdateGIData + drawCUDA one frame at a time.  Full-size shares
+    exercise what the 128^3 cases cannot: 2,040 tiles with padded weighted slices, 16-frame groups
+    carrying whole-size GI windows, 33 MB RGB24 gather buffers.  C5's ranks run without the texture
+    tile table (32 GiB each at 2048^3; the tiles are the same either way)."""
+    from rvgrt_amd.configs import CONFIGS, camera_path, pose_f32
+    cfg = CONFIGS[cfgname]
+    if cfgname == "c5":
+        monkeypatch.setenv("RV_TEX_TABLE", "0")
+    W, H = cfg.width, cfg.height
+    seq = camera_path(pose_f32(cfg, "P0"), W, H, 21, pan=0.0005, ref_compat=True)
+
+    def make():
+        r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=atlas)
+        r.world_build()
+        for s in range(cfg.gi_sweeps):
+            r.gi_update(s)
+        return r
+
+    ref = make()
+    ref.set_pipeline(0)
+    group = rv.LoopbackGroup(N, timeout_ms=120000)
+    rs = [make() for _ in range(N)]
+    comms = []
+    for q, r in enumerate(rs):
+        r.set_tile_shard(64, q, N, root_weight=w0)
+        r.set_gather_bpp(3)
+        r.set_frame_group(grp)
+        comms.append(rv.Comm.loopback(r, group, q))
+    if grp:
+        assert rs[0].frame_group_effective() == grp
+    done = 0
+    for a, b, nxt in ((0, 17, 17), (17, 20, None)):
+        _run_ranks([lambda q=q: rs[q].render_frame_seq(seq[a:b], next_desc=seq[nxt] if nxt else None,
+                                                       flags=cfg.flags, gi_per_frame=True, comm=comms[q])
+                    for q in range(N)])
+        for c in comms:
+            c.wait(120000)
+        for k in range(done, b):
+            ref.update_gi_data()
+            d = seq[k]
+            ref.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time,
+                      jx=d.jitter_x, jy=d.jitter_y, flags=cfg.flags)
+        done = b
+        assert np.array_equal(rs[0].readback(rv.RV_IMAGE_COLOR), ref.readback(rv.RV_IMAGE_COLOR)), (a, b)
+        want = ref.world_export(rv.RV_WORLD_GI)
+        for q, r in enumerate(rs):
+            assert np.array_equal(r.world_export(rv.RV_WORLD_GI), want), (q, a, b)
+    for c in comms:
+        c.close()
+    for r in rs:
+        r.close()
+    group.close()
+    ref.close()

@@ -211,3 +211,57 @@ def test_sun_exit_keeps_every_shadow_hit(host_lib, oracle_world, g8, sky):
     assert 0.1 < o["hit"].mean() < 0.9                      # shadowed and lit points both
     assert g["sphere"].sum() < 0.8 * o["n_sphere"].sum()    # the horizon does cut the march
     assert hz.min() < hz.max()                               # the horizon varies over the terrain
+
+
+@pytest.mark.parametrize("g8", [0, 1])
+def test_column_skip_keeps_every_hit(host_lib, g8):
+    """The DDA's empty-column skip (trace COL = true, rv_device.h; the water reflections of the pipelined
+    and grouped launches): a look-ahead group whose lowest row is at or above the highest solid row of the
+    3x3 brick columns around its first cell issues no voxel gathers.  Rays that skim just above the terrain
+    -- ascending, level and descending (the iy - G bound), from the surface tops and from the water plane
+    at grazing angles -- give the same hit, position, normal, uv and step counts as the same traversal
+    without the skip (both with the sky exit and the dtop table built as rv_abi.cpp's world_top builds
+    it), and the oracle's hits; the skip must fire on a good share of the groups."""
+    from oracle import oracle as O
+    L = host_lib
+    L.rvh_trace_col.restype = C.c_int
+    L.rvh_trace_col.argtypes = [C.c_int] * 5 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p]
+    ow = O.OracleWorld(7, 7, 7).build(gi_sweeps=-1)
+    vox = ow.voxels()                                         # [z, y, x]
+    top = np.where(vox.any(axis=1), ow.Y - 1 - np.argmax(vox[:, ::-1, :], axis=1), 0)   # highest solid y per (z, x)
+    rng = np.random.default_rng(21)
+    n = 12000
+    x = rng.integers(0, ow.X, n)
+    z = rng.integers(0, ow.Z, n)
+    org = np.stack([x + rng.uniform(0, 1, n), top[z, x] + 1 + rng.uniform(0.05, 4.0, n), z + rng.uniform(0, 1, n)],
+                   1).astype(np.float32)
+    water = rng.uniform(size=n) < 0.3                         # reflection-like starts on the water plane
+    org[water, 1] = np.float32(31.0) + rng.uniform(0.0, 1.0, water.sum()).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[:, 1] = rng.uniform(-0.25, 0.25, n) * np.hypot(d[:, 0], d[:, 2])   # grazing, up and down
+    d[rng.uniform(size=n) < 0.05, 1] = 0.0                                 # exactly level
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    dist = np.zeros(n, np.float32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731
+    out = []
+    for col in (1, 0):
+        g = np.zeros(n, HIT)
+        assert L.rvh_trace_col(g8, col, ow.lx, ow.ly, ow.lz, p(ow.bits), p(ow.csdf), p(np.ascontiguousarray(org)),
+                               p(np.ascontiguousarray(d)), p(dist), n, p(g)) == 0
+        out.append(g)
+    a, b = out
+    for k in ("hit", "undef", "sphere", "dda", "check"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in ("pos", "normal", "u", "v"):
+        assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
+    o = ow.trace_batch(org, d, dist)
+    assert np.array_equal(a["hit"], o["hit"]) and np.array_equal(a["undef"], o["undef"])
+    assert np.array_equal(a["pos"].view(np.uint32), o["pos"].view(np.uint32))
+    assert np.array_equal(a["normal"], o["normal"])
+    assert np.array_equal(a["u"].view(np.uint32), o["u"].view(np.uint32))
+    assert np.array_equal(a["v"].view(np.uint32), o["v"].view(np.uint32))
+    skipped = a["pad"].sum()                                    # col_skip: groups known empty
+    groups = (a["dda"].astype(np.int64) + (8 if g8 else 4) - 1) // (8 if g8 else 4)
+    assert b["pad"].sum() == 0 and skipped > 0.05 * groups.sum(), (skipped, groups.sum())
+    desc = d[:, 1] < 0
+    assert a["pad"][desc].sum() > 0 and a["pad"][~desc].sum() > 0   # both branches of the row bound fire

@@ -1,0 +1,107 @@
+#!/usr/bin/env bash
+# One measurement script for the GPU box (run through gpurun from the repo root), replacing the per-round
+# one-off recipes.  Every GPU step runs under its own time limit; the first failure ends the script.
+#
+#   tools/measure.sh tests [pytest -k expr]        the -m gpu suite            -> gpurun_out/<TAG>_tests.log
+#   tools/measure.sh bench NAME:ARGS ...           bench lines (ARGS with _ for spaces, e.g.
+#                                                  c4_P1:--config_c4_--pose_P1)  -> gpurun_out/<TAG>_bench_NAME.json
+#   tools/measure.sh pmc CFG:POSE:KERNEL:FPL:LOOP  PMC passes (FETCH_SIZE, WRITE_SIZE, then TA/TD/TCP/SQ) of the
+#                                                  same bench loop; tools/pmc_summary.py -> profiles/traffic_*.json
+#   tools/measure.sh prof [NAME:ARGS ...]          rocprofv3 --kernel-trace --stats of bench lines
+#                                                  (default: the driver's bench and the drop-in loop)
+#                                                  -> gpurun_out/<TAG>_prof_NAME/
+#   tools/measure.sh ab REPS NAME:ENV:ARGS ...     alternating A/B runs (ENV: VAR=v,VAR2=w or -; ARGS as above),
+#                                                  REPS rounds, ms/frame of each        -> gpurun_out/<TAG>_ab.txt
+#   tools/measure.sh shard CFG GROUP [NS]          slowest rank share per N (tools/shard_probe.py, 64-px tiles,
+#                                                  GI shard, no exchange)               -> gpurun_out/<TAG>_shard.txt
+# TAG (env, default r05) prefixes every output; STEPS/WARMUP (env) size the bench runs (default 200/20).
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+TAG=${TAG:-r05}
+STEPS=${STEPS:-200}
+WARMUP=${WARMUP:-20}
+cmd=$1; shift
+
+run() {   # run NAME LIMIT cmd...: output to gpurun_out/TAG_NAME.log, stop the script on failure
+    local name=$1 lim=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1 || {
+        echo "FAILED $name rc=$?"; tail -8 "gpurun_out/${TAG}_$name.log"; exit 3; }
+}
+
+summary() {   # one line per bench JSON
+    python3 - "$1" "$2" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+rf = d["roofline"]; lim = rf.get("limit") or {}
+di = d.get("dropin") or {}
+print(sys.argv[1], d["ms_per_step"], "ms/frame,", "lat", d["latency_ms"], "|", rf["kernel"], "frac", rf["frac"],
+      "td", lim.get("td_busy"), "| dropin", di.get("ms_per_step"), di.get("latency_ms"),
+      (di.get("roofline") or {}).get("frac"))
+EOF
+}
+
+case "$cmd" in
+tests)
+    k=${1:+-k "$1"}
+    run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $k
+    tail -3 "gpurun_out/${TAG}_tests.log" ;;
+bench)
+    for spec in "$@"; do
+        name=${spec%%:*}; args=$(echo "${spec#*:}" | tr '_' ' ')
+        run "bench_$name" 300 python bench.py $args --steps "$STEPS" --warmup "$WARMUP"
+        grep '^{' "gpurun_out/${TAG}_bench_$name.log" | tail -1 > "gpurun_out/${TAG}_bench_$name.json"
+        summary "$name" "gpurun_out/${TAG}_bench_$name.json"
+    done ;;
+pmc)
+    for spec in "$@"; do
+        IFS=: read -r c pose kern fpl loop <<< "$spec"
+        suf=""; [ "$pose" != P0 ] && suf=_$pose; [ "$loop" = drawcuda ] && suf=${suf}_drawcuda
+        t=${c}${suf}
+        for set in "FETCH_SIZE" "WRITE_SIZE" \
+                   "TA_TA_BUSY_sum TD_TD_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"; do
+            first=${set%% *}
+            rm -rf "gpurun_out/pmc_${TAG}${t}_$first"
+            echo "== pmc $t $first ($(date +%T))"
+            timeout -s KILL 150 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "gpurun_out/pmc_${TAG}${t}_$first" \
+                -o run -- python3 bench.py --config "$c" --pose "$pose" --loop "$loop" --steps 32 --warmup 8 \
+                --cpu-seconds 0 --dropin-leg 0 > "gpurun_out/${TAG}_pmc_${t}_$first.log" 2>&1 || {
+                echo "FAILED pmc $t $first"; tail -3 "gpurun_out/${TAG}_pmc_${t}_$first.log"; exit 3; }
+        done
+        python3 tools/pmc_summary.py --prefix "${TAG}${t}_" --config "$c$suf" --kernel "$kern" --fpl "$fpl" --grid -1 \
+            --out "gpurun_out/traffic_$c$suf.json" && cp "gpurun_out/traffic_$c$suf.json" "profiles/traffic_$c$suf.json"
+    done ;;
+prof)
+    [ $# -eq 0 ] && set -- "c4:--steps_20_--warmup_5" "dc_c4:--loop_drawcuda_--steps_20_--warmup_5"
+    for spec in "$@"; do
+        name=${spec%%:*}; args=$(echo "${spec#*:}" | tr '_' ' ')
+        rm -rf "gpurun_out/${TAG}_prof_$name"
+        run "prof_$name" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${TAG}_prof_$name" -o run \
+            -- python3 bench.py $args --cpu-seconds 0
+        grep '^{' "gpurun_out/${TAG}_prof_$name.log" | tail -1 > "gpurun_out/${TAG}_prof_$name/bench_line.json"
+    done ;;
+ab)
+    reps=$1; shift
+    out="gpurun_out/${TAG}_ab.txt"
+    for ((i = 0; i < reps; i++)); do
+        for spec in "$@"; do
+            IFS=: read -r name envs args <<< "$spec"
+            args=$(echo "$args" | tr '_' ' ')
+            envv=(); [ "$envs" != "-" ] && IFS=, read -r -a envv <<< "$envs"
+            run "ab_$name" 300 env "${envv[@]}" python bench.py $args --steps "$STEPS" --warmup "$WARMUP" --cpu-seconds 0 \
+                --dropin-leg 0
+            ms=$(grep '^{' "gpurun_out/${TAG}_ab_$name.log" | tail -1 | python3 -c \
+                 "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['roofline']['avg_launch_ms'], d['latency_ms'])")
+            echo "$i $name ${envs} ${args} :: ms/frame launch_ms latency_ms = $ms" | tee -a "$out"
+        done
+    done ;;
+shard)
+    c=$1; g=$2; ns=${3:-2,4,8}
+    echo "== shard $c group $g ($(date +%T))" | tee -a "gpurun_out/${TAG}_shard.txt"
+    SHARD_GROUP=$g SHARD_NS=$ns RV_GI_SHARD_PROBE=1 timeout -k 10 500 python tools/shard_probe.py "$c" 1 64 \
+        > "gpurun_out/${TAG}_shard_${c}_$g.log" 2>&1 || { echo "FAILED shard"; tail -5 "gpurun_out/${TAG}_shard_${c}_$g.log"; exit 3; }
+    grep -v "frames \.\.\.\|amdgpu.ids" "gpurun_out/${TAG}_shard_${c}_$g.log" | tee -a "gpurun_out/${TAG}_shard.txt" ;;
+*)
+    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard ..."; exit 2 ;;
+esac

@@ -3,7 +3,7 @@
 (k_ref_pipe: GI update | pre-pass | render), for a whole frame or one rank's
 tile share, on ONE GPU: the latency floor of a launch.  Needs
 a library built with -DRV_PIPE_DIAG=1 (RVGRT_LIB=rvgrt_amd/variants/diag/...,
-see tools/gpu_run.sh `waves`) and RV_PIPE_WAVE_STATS=1 (the library prints the
+see DESIGN.md s7) and RV_PIPE_WAVE_STATS=1 (the library prints the
 table when the context is destroyed); for shares RV_GI_SHARD_PROBE=1.  Not
 part of the product.
 

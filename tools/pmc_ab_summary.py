@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One line per A/B run of tools/r03_pmc_ab.sh: bench ms/frame and the dominant kernel's
+"""One line per A/B run of PMC passes (tools/measure.sh pmc): bench ms/frame and the dominant kernel's
 counters per launch (gpurun_out/pab_<tag>.json, gpurun_out/pmcab_<tag>/*counter_collection.csv).
 TD busy = TD_TD_BUSY_sum / (256 TDs x GRBM_GUI_ACTIVE / 8): GRBM_GUI_ACTIVE sums the 8 XCDs' cycles
 (9.8 M for a 0.49-ms C4 launch at 2.4 GHz, profiles/traffic_c4.json)."""

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--kernel", default="k_render<false")
     ap.add_argument("--out", default=None)
     ap.add_argument("--fpl", type=int, default=8, help="frames per launch of the profiled bench run")
-    ap.add_argument("--prefix", default="", help="pass directories pmc_<prefix>* only (gpu_run.sh PMC_TAG)")
+    ap.add_argument("--prefix", default="", help="pass directories pmc_<prefix>* only (tools/measure.sh pmc: TAG + config)")
     ap.add_argument("--grid", type=int, default=0, help="dispatches of this Grid_Size only (-1: the largest, i.e. the full-group launches)")
     a = ap.parse_args()
     vals = collections.defaultdict(list)
