@@ -20,6 +20,9 @@
 #include <vector>
 
 #include "../../include/rvgrt/rv_frame.h"
+#ifndef RV_PIPE_DIAG
+#define RV_PIPE_DIAG 0   // per-wave diagnostics of the pipelined and flow launches (tools/pipe_waves.py, tools/flow_waves.py)
+#endif
 
 using namespace rv;
 
@@ -140,6 +143,9 @@ struct rv_ctx {
     uint64_t pipe_chunk = 0; int pipe_chunk_n = 0;
     hipEvent_t pipe_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // rendered, all-gathered, gathered[2]
     uint32_t* pipe_wstat = nullptr;   // env RV_PIPE_WAVE_STATS: per-wave records of the first launches
+    // env RV_FLOW_WAVE_TRACE=<file> (RV_PIPE_DIAG builds): the last flow launch's per-wave records, dumped at
+    // rv_destroy (tools/flow_waves.py)
+    uint32_t* flow_wtrace = nullptr; uint32_t flow_wtrace_n = 0, flow_wlen[3] = {0, 0, 0};
     uint32_t pipe_launches = 0;
     uint32_t pipe_wnb[64] = {};       // workgroups of each recorded launch
     int gather_bpp = 3;           // RV_GATHER_BPP: packed pixel bytes of rv_render_frames' tile gather (3 or 4)
@@ -188,6 +194,10 @@ struct rv_ctx {
     // render waves read are published first (C3 -2 %, C4 -0.2 %, render waves finding a tile unpublished
     // on arrival 330 -> 130 per C4 frame: profiles/r04/flow_ab.txt); 0 the pre-pass's own cost order
     uint32_t flow_pp_order = 1;
+    // env RV_FLOW_GI_SIDE=1: the next UpdateGIData's cells of a flow frame run as their own GI kernel on the
+    // low-priority GI stream beside the flow launch (which then holds pre-pass + render only) instead of as
+    // the flow launch's GI part; same cells, same kernel body, consumed the same way (ev_spec)
+    bool flow_gi_side = false;
     // The next UpdateGIData computed ahead by a flow launch (camera-independent): update `spec_fr` of
     // [spec_first, + spec_count) in gi_tmp, valid while the world/GI version is spec_world; recorded
     // on the launch's stream (ev_spec).  upd_since_frame: an UpdateGIData came since the last frame
@@ -417,6 +427,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     if (const char* e = getenv("RV_FLOW_SPIN")) c->flow_spin = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("RV_FLOW_FORCE_FALLBACK")) c->flow_force_fallback = atoi(e) != 0;
     if (const char* e = getenv("RV_FLOW_PP_ORDER")) c->flow_pp_order = (uint32_t)(atoi(e) != 0);
+    if (const char* e = getenv("RV_FLOW_GI_SIDE")) c->flow_gi_side = atoi(e) != 0;
     if (const char* e = getenv("RV_GROUP")) c->group = std::min(32, std::max(0, atoi(e)));
     if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
         if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
@@ -471,6 +482,13 @@ void rv_destroy(rv_ctx* c) {
     for (int q = 0; q < 2; q++) { hipFree(c->pipe_tbuf[q]); hipFree(c->pipe_gbuf[q]); }
     hipFree(c->pipe_gi_stage); hipFree(c->pipe_gi_all);
     for (hipEvent_t e : c->pipe_ev) if (e) hipEventDestroy(e);
+    if (c->flow_wtrace) {   // RV_FLOW_WAVE_TRACE: header {len0, len1, len2, n}, then 4 dwords per workgroup
+        std::vector<uint32_t> h((size_t)c->flow_wtrace_n * 4 + 4);
+        h[0] = c->flow_wlen[0]; h[1] = c->flow_wlen[1]; h[2] = c->flow_wlen[2]; h[3] = c->flow_wtrace_n;
+        if (hipMemcpy(h.data() + 4, c->flow_wtrace, (size_t)c->flow_wtrace_n * 16, hipMemcpyDeviceToHost) == hipSuccess)
+            if (FILE* fp = fopen(getenv("RV_FLOW_WAVE_TRACE"), "wb")) { fwrite(h.data(), 4, h.size(), fp); fclose(fp); }
+        hipFree(c->flow_wtrace);
+    }
     if (c->pipe_wstat) {   // RV_PIPE_WAVE_STATS: per part, the longest wave and the 99th percentile per launch
         const char* names[3] = {"gi", "prepass", "render"};
         double mx[3] = {0, 0, 0}, p99[3] = {0, 0, 0};
@@ -1244,12 +1262,37 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     p.len[0] = c->flow_pp_order ? n_chunks_pad(f.W, f.H) * 16u : pipe_len(f, PIPE_PP, 0);
     p.len[2] = pipe_len(f, PIPE_RENDER, 0);
     p.gi_pairs = c->gi_pairs > 0 && pipe_latency_variant(f, p.len[2]) ? 1u : 0u;   // whole frames: off unless forced
-    p.len[1] = spec ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * count : count) : 0u;
+    const bool side = spec && c->flow_gi_side && c->gi_stream;
+    p.len[1] = spec && !side ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * count : count) : 0u;
+    if (side) {
+        // the GI stream starts once the grid this frame renders with is complete (every earlier write of
+        // `gi` and gi_tmp on the frame stream: the last copy-back included), then computes the window
+        // into gi_tmp beside the flow launch; the next rv_update_gi_data waits for ev_spec
+        if (!c->ev_spec) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->ev_spec, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->gi_stream, c->ev_spec, 0));
+        launch_gi_update(c->gi_stream, c->gi, c->gi_tmp, current_world(c), sun_dir(), c->gi_frame, first, count,
+                         c->counters + ST_GI * NCNT, false);
+        LAUNCH_CHECK(c);
+    }
     p.flow_half = c->flow_half;
     p.flow_epoch = c->flow_epoch; p.flow_ntx = ntx;
     p.flow_expect = c->flow_force_fallback ? c->flow_epoch ^ 0x40000000u : c->flow_epoch;
     p.flow_spin = c->flow_spin;
     p.flow_fallback = c->flow_fb;
+    if (RV_PIPE_DIAG && getenv("RV_FLOW_WAVE_TRACE")) {   // diagnostics: this launch's per-wave records
+        const uint32_t nb = p.len[0] + p.len[1] + p.len[2];
+        if (nb > c->flow_wtrace_n) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            hipFree(c->flow_wtrace);
+            c->flow_wtrace = nullptr;
+            HIP_TRY(c, hipMalloc(&c->flow_wtrace, (size_t)nb * 16));
+        }
+        c->flow_wtrace_n = nb;
+        c->flow_wlen[0] = p.len[0]; c->flow_wlen[1] = p.len[1]; c->flow_wlen[2] = p.len[2];
+        HIP_TRY(c, hipMemsetAsync(c->flow_wtrace, 0xFF, (size_t)nb * 16, c->stream));
+        p.wave_max = c->flow_wtrace;
+    }
     const bool timed = c->timing_n < c->timing_cap;
     const size_t e0 = (size_t)EV_PER_FRAME * c->timing_n;
     if (timed) { c->ev_stage[e0] = ST_PRIMARY; HIP_TRY(c, hipEventRecord(c->ev[e0], c->stream)); }
@@ -1266,8 +1309,8 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     }
     if (spec) {
         if (!c->ev_spec) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
-        HIP_TRY(c, hipEventRecord(c->ev_spec, c->stream));
-        c->spec_stream = c->stream;
+        HIP_TRY(c, hipEventRecord(c->ev_spec, side ? c->gi_stream : c->stream));
+        c->spec_stream = side ? c->gi_stream : c->stream;
         c->spec_rec = true;
         c->spec_gi = true;
         c->spec_fr = c->gi_frame; c->spec_first = first; c->spec_count = count; c->spec_world = c->world_ver;
@@ -2031,9 +2074,6 @@ static rv_status render_gi_groups(rv_ctx* c, const Seq& q, int32_t flags, hipStr
 // frame k+1 renders; rank 0 assembles frame k after launching frame k+1.
 // Without a communicator an N > 1 shard renders its share only (its GI part
 // covers the whole window, so its grid stays the reference's).
-#ifndef RV_PIPE_DIAG
-#define RV_PIPE_DIAG 0   // per-wave diagnostics of the pipelined launch (tools/pipe_waves.py builds it)
-#endif
 constexpr uint32_t PIPE_WSTAT_N = 32, PIPE_WSTAT_MAXB = 1u << 18;   // launches, workgroups per launch
 
 // What a kept pre-pass was computed for: the camera fields the pre-pass

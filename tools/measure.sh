@@ -44,8 +44,8 @@ EOF
 
 case "$cmd" in
 tests)
-    k=${1:+-k "$1"}
-    run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $k
+    kargs=(); [ -n "$1" ] && kargs=(-k "$1")
+    run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${kargs[@]}"
     tail -3 "gpurun_out/${TAG}_tests.log" ;;
 bench)
     for spec in "$@"; do
