@@ -144,13 +144,32 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // (other resolutions) reads the image.
 struct HalfWin {
     const float* d;   // LDS: 64 distance texels, row-major 8x8 (nullptr: no window)
-    const float* s;   // LDS: 64 shadow texels
+    const float* s;   // LDS: 64 shadow texels (SHADOW_PENDING: not published yet, flow launches only)
     int ox, oy;
+    // flow launches (k_ref_flow): the tagged granules the window came from, for the shadow texels that were
+    // still pending when the wave loaded its window (resolve_shadow_taps)
+    const uint64_t* gran;
+    uint32_t ntx;     // granule tiles per row
+    uint32_t want;    // the launch's epoch (30 bits)
 };
+// A shadow texel whose pre-pass lane has published its distance but not yet its shadow (flow launches:
+// the two-phase hand-off); never a value of the image (1 or SHADOW_HIT).
+static constexpr float SHADOW_PENDING = -1.0f;
+// Flow granule: {distance bits, shadow-hit bit, tag} with tag = epoch << 1 | phase in bits 33..63; phase 0
+// carries the distance only (published after the camera ray), phase 1 the distance and the shadow (after
+// the shadow ray).
+__device__ __forceinline__ uint64_t flow_granule(float d, float s, uint32_t epoch, uint32_t phase) {
+    return (uint64_t)__float_as_uint(d) | ((uint64_t)(s != 1.0f) << 32) |
+           ((uint64_t)(((epoch & 0x3FFFFFFFu) << 1) | phase) << 33);
+}
+__device__ __forceinline__ size_t flow_granule_index(uint32_t ntx, int tx, int ty) {
+    return (size_t)((uint32_t)(ty >> 3) * ntx + (uint32_t)(tx >> 3)) * 64 + (uint32_t)(ty & 7) * 8 + (uint32_t)(tx & 7);
+}
 // All 64 lanes of the wave call this (before any per-pixel branch): lane l
 // loads texel (l & 7, l >> 3).  lds holds 128 floats for this wave.
 __device__ __forceinline__ HalfWin half_window_load(const FrameParams& f, int X0, int Y0, float* lds) {
     HalfWin hw;
+    hw.gran = nullptr; hw.ntx = 0; hw.want = 0;
     hw.ox = (X0 >> 1) - 2;
     hw.oy = (Y0 >> 1) - 2;
     const int l = (int)(threadIdx.x & 63u);
@@ -198,6 +217,30 @@ __device__ __forceinline__ float min_dist(const FrameParams& f, float x, float y
     float d1 = half_tap(hd, win, f, ox, oy, u, v), d2 = half_tap(hd, win, f, ox, oy, u1, v);
     float d3 = half_tap(hd, win, f, ox, oy, u, v1), d4 = half_tap(hd, win, f, ox, oy, u1, v1);
     return fminf(fminf(d1, d2), fminf(d3, d4));
+}
+
+// Flow launches: the shadow texels of this lane's 4 bilinear taps (bilinear_tex's indices) that were still
+// pending when the window was loaded, read from their granules once their pre-pass lane has published
+// the shadow (phase 1) and written back to the window.  The wait needs no bound: a pending texel's
+// distance was published by its pre-pass wave, which is therefore running, never waits and publishes the
+// shadow next (texels the render wave evaluated itself are never pending).
+__device__ __forceinline__ void resolve_shadow_taps(const FrameParams& f, float x, float y, const HalfWin* hwin) {
+    if (!hwin || !hwin->gran) return;
+    float xb = x * (float)f.hw - 0.5f, yb = y * (float)f.hh - 0.5f;
+    const int i0 = (int)floorf(xb), j0 = (int)floorf(yb);
+    float* win = const_cast<float*>(hwin->s);
+    const uint64_t want = ((uint64_t)hwin->want << 1) | 1u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ru = i0 + (k & 1), rv = j0 + (k >> 1);
+        const int wx = ru - hwin->ox, wy = rv - hwin->oy;
+        if ((uint32_t)wx >= 8u || (uint32_t)wy >= 8u || win[wy * 8 + wx] != SHADOW_PENDING) continue;
+        const uint64_t* g = hwin->gran + flow_granule_index(hwin->ntx, clampi(ru, 0, f.hw - 1), clampi(rv, 0, f.hh - 1));
+        uint64_t v;
+        while (((v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 33) != want)
+            __builtin_amdgcn_s_sleep(8);
+        win[wy * 8 + wx] = ((v >> 32) & 1u) ? SHADOW_HIT : 1.0f;
+    }
 }
 
 // tex2D<float> linear/clamp/normalized with 1/256 weights (StateRender.cu:230)

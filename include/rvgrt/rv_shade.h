@@ -55,9 +55,13 @@ namespace rv {
 // one half-res pixel of distApproximationKernel (StateRender.cu:255-286): its distance (d - 8, the
 // value stored) and shadow texels
 // G: the traversal's DDA look-ahead (every G gives the same hit: rv_device.h trace)
-template <bool STATS, class WV = World, int G = RV_G_PREPASS>
+struct NoPublish { __device__ void operator()(float) const {} };
+// on_dist(d - 8): called once the camera ray is done, before the shadow ray (the flow launch publishes the
+// distance there: the two-phase hand-off, rv_kernels.hip flow_pre_part)
+template <bool STATS, class WV = World, int G = RV_G_PREPASS, class PUB = NoPublish>
 __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, int ix, int iy,
-                                             uint32_t (&c)[NCNT], float& dist_out, float& shadow_out) {
+                                             uint32_t (&c)[NCNT], float& dist_out, float& shadow_out,
+                                             const PUB& on_dist = PUB()) {
     float x = ((float)ix + 0.5f) / (float)f.hw;
     float y = ((float)iy + 0.5f) / (float)f.hh;
     f3 dir = ray_dir(f, x, y);
@@ -67,6 +71,7 @@ __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, 
         w, f.pos, dir, 0.0f, sc);
     float d = h.hit ? length(sub(h.pos, f.pos)) : 300.0f;
     float s = 1.0f;
+    on_dist(d - 8.0f);
     if (STATS) { c[CNT_TRACES]++; c[CNT_PP_PRIMARY]++; c[CNT_UNDEF] += h.undef; }
     if (h.hit && !(RV_ABLATE & 1024)) {
         RV_GD_KIND(gd::PP_SHADOW);
@@ -126,9 +131,14 @@ template <uint32_t FEAT> struct TraceCfg {
 // computeColor (StateRender.cu:33-146)
 // COLOK: the launch may take the water reflection's column skip (k_ref_flow: no -- its render waits inside
 // the launch and the skip's registers cost it 3.5 %, profiles/r04/col_skip_atlas_ab.txt)
-template <bool STATS, uint32_t FEAT, int CB = RV_CONE_GROUP, int GR = 0, class WV = World, bool COLOK = true>
+// DS (k_ref_flow): the pre-pass shadow is fetched only where the land branch uses it, after the cones
+// (bilinear_tex over hwin once resolve_shadow_taps has its texels): the render's primary and secondary
+// rays run while the pre-pass lanes still trace their shadow rays.  Same arithmetic either way.
+template <bool STATS, uint32_t FEAT, int CB = RV_CONE_GROUP, int GR = 0, class WV = World, bool COLOK = true,
+          bool DS = false>
 __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, float x, float y,
-                                            float dist, float shadow_in, Hit& hit, uint32_t (&c)[NCNT]) {
+                                            float dist, float shadow_in, Hit& hit, uint32_t (&c)[NCNT],
+                                            const HalfWin* hwin = nullptr) {
     const bool prepass = has<FEAT>(f, RV_F_PREPASS);
     f3 dir = ray_dir(f, x, y);
     StepCount sc{};
@@ -203,6 +213,33 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         f3 base = sample_texture(w, hit.u, hit.v, hit.pos);
         if (STATS) c[CNT_TEX]++;
         float shadow = shadow_in;
+        if (DS && has<FEAT>(f, RV_F_GI) && !(RV_ABLATE & 2)) {   // the cones first, then the deferred shadow
+            float diffuse = fmaxf(dot(hit.normal, f.sun), 0.0f);
+            f3 up = hit.normal;
+            f3 right, fwd;
+            if ((up.x != 0.0f) | (up.y != 0.0f) | (up.z != 0.0f)) {
+                right = scale(cross(up, V(0.577f, 0.577f, 0.577f)), f.cone_k1);
+                fwd = scale(cross(up, right), f.cone_k2);
+            } else {
+                right = normalize(cross(up, V(0.577f, 0.577f, 0.577f)));
+                fwd = normalize(cross(up, right));
+            }
+            uint32_t steps = 0;
+            f3 ind = trace_cones6<STATS, CB>(w, hit.pos, up, right, fwd, steps);
+            if (STATS) { c[CNT_CONES] += 6; c[CNT_CONE_STEPS] += steps; }
+            ind = scale(mul(divs(ind, 6.0f), base), 0.6f);
+            f3 amb = mul(scale(sample_sky(hit.normal, f.sun), 0.05f), base);
+            if (prepass) {
+                resolve_shadow_taps(f, x, y, hwin);
+                shadow = bilinear_tex(f, x, y, hwin);
+            }
+            f3 direct = scale(scale(base, diffuse), shadow);
+            color = add(add(direct, ind), amb);
+        } else {
+        if (DS && prepass) {
+            resolve_shadow_taps(f, x, y, hwin);
+            shadow = bilinear_tex(f, x, y, hwin);
+        }
         if (!prepass) {
             shadow = 1.0f;
             if (has<FEAT>(f, RV_F_SHADOW)) {
@@ -244,6 +281,7 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         } else {
             color = direct;
         }
+        }
     } else {
         color = sample_sky(dir, f.sun);
     }
@@ -276,17 +314,17 @@ __device__ __forceinline__ void clip_pos(const float* P, const float* M, f3 p, f
 
 // renderKernel body for one pixel (StateRender.cu:200-253); returns RGBA8
 template <bool STATS, uint32_t FEAT, bool CAMS = false, bool LATE = false, int CB = RV_CONE_GROUP, int GR = 0,
-          class WV = World, bool COLOK = true>
+          class WV = World, bool COLOK = true, bool DS = false>
 __device__ __forceinline__ uint32_t render_pixel(const WV& w, const FrameParams& f, int ix, int iy,
                                                  uint32_t (&c)[NCNT], const HalfWin* hwin = nullptr) {
     float x = (float)ix / (float)f.W, y = (float)iy / (float)f.H;
     float dist = 0.0f, shadow = 1.0f;
     if (has<FEAT>(f, RV_F_PREPASS)) {
         dist = min_dist(f, x, y, hwin);
-        shadow = bilinear_tex(f, x, y, hwin);
+        if (!DS) shadow = bilinear_tex(f, x, y, hwin);   // DS: where the land branch uses it (compute_color)
     }
     Hit h;
-    f3 col = compute_color<STATS, FEAT, CB, GR, WV, COLOK>(w, f, x, y, dist, shadow, h, c);
+    f3 col = compute_color<STATS, FEAT, CB, GR, WV, COLOK, DS>(w, f, x, y, dist, shadow, h, c, hwin);
     float mvx = 0.0f, mvy = 0.0f, dep = 1.0f;
     if (h.hit) {   // mat_mul_vec (cumath.cuh:47-54), glm column-major
         float pc[4], cc[4];

@@ -1234,7 +1234,7 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
         HIP_TRY(c, hipMalloc(&c->flow_fb, 8));
         HIP_TRY(c, hipMemset(c->flow_fb, 0, 8));
     }
-    if (++c->flow_epoch > 0x7FFFFFFFu) {   // 31-bit tags: restart the epochs from a zeroed buffer
+    if (++c->flow_epoch > 0x3FFFFFFFu) {   // 30-bit epochs (tag = epoch << 1 | phase): restart them from a zeroed buffer
         HIP_TRY(c, hipMemsetAsync(c->flow_half, 0, ntiles * 64 * 8, c->stream));
         c->flow_epoch = 1;
     }
@@ -1277,7 +1277,7 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     }
     p.flow_half = c->flow_half;
     p.flow_epoch = c->flow_epoch; p.flow_ntx = ntx;
-    p.flow_expect = c->flow_force_fallback ? c->flow_epoch ^ 0x40000000u : c->flow_epoch;
+    p.flow_expect = c->flow_force_fallback ? c->flow_epoch ^ 0x20000000u : c->flow_epoch;
     p.flow_spin = c->flow_spin;
     p.flow_fallback = c->flow_fb;
     if (RV_PIPE_DIAG && getenv("RV_FLOW_WAVE_TRACE")) {   // diagnostics: this launch's per-wave records
