@@ -1258,6 +1258,7 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
     p.part[0] = PIPE_PP; p.part[1] = PIPE_GI; p.part[2] = PIPE_RENDER;
     p.flow_pp_by_render = c->flow_pp_order;
+    if (const char* e = getenv("RV_FLOW_OPTS")) p.flow_opts = (uint32_t)atoi(e);   // A/B experiments
     // pre-pass workgroups: 16 per render chunk slot in the render's order, or the pre-pass's own grid
     p.len[0] = c->flow_pp_order ? n_chunks_pad(f.W, f.H) * 16u : pipe_len(f, PIPE_PP, 0);
     p.len[2] = pipe_len(f, PIPE_RENDER, 0);

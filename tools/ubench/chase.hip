@@ -1,0 +1,77 @@
+// Micro-benchmark: latency of one dependent gather on gfx950 by where the line lives -- the floor of a
+// lone ray's chain (a sphere step's next address is its gather's result).  One lane chases a random
+// cyclic permutation of 128-B lines over a buffer of S bytes (S from L2-resident to far beyond the
+// 256 MB Infinity Cache), optionally while every other CU streams through a separate buffer (the load
+// the tail of a frame launch runs under).  Prints ns per hop.  Not part of the product.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <random>
+#include <algorithm>
+
+__global__ void k_chase(const unsigned* __restrict__ buf, unsigned start, int hops, unsigned* out,
+                        unsigned long long* ticks) {
+    if (threadIdx.x != 0) return;
+    unsigned p = start;
+    const unsigned long long t0 = __builtin_readcyclecounter();
+    const unsigned long long r0 = wall_clock64();
+    for (int i = 0; i < hops; i++) p = buf[p];
+    const unsigned long long r1 = wall_clock64();
+    const unsigned long long t1 = __builtin_readcyclecounter();
+    out[0] = p;
+    ticks[0] = r1 - r0;
+    ticks[1] = t1 - t0;
+}
+
+// background load: each wave streams a private slice (coalesced dword loads), until *stop is set
+__global__ void k_load(const unsigned* __restrict__ buf, size_t n, volatile unsigned* stop, unsigned* out) {
+    unsigned acc = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (int rep = 0; rep < 8000 && !*stop; rep++)
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride * 64) acc += buf[i];
+    if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
+int main(int argc, char** argv) {
+    const bool loaded = argc > 1 && atoi(argv[1]) != 0;
+    const size_t sizes[] = {1u << 20, 4u << 20, 16u << 20, 64u << 20, 128u << 20, 256u << 20, 1024u << 20};
+    unsigned *out, *stop, *lbuf = nullptr;
+    unsigned long long* ticks;
+    hipMalloc(&out, 16);
+    hipMalloc(&ticks, 16);
+    hipHostMalloc(&stop, 4, hipHostMallocCoherent);
+    const size_t ln = (size_t)512 << 20;   // 2 GiB background buffer
+    if (loaded) { hipMalloc(&lbuf, ln * 4); hipMemset(lbuf, 1, ln * 4); }
+    hipStream_t sl, sc;
+    hipStreamCreateWithFlags(&sl, hipStreamNonBlocking);
+    hipStreamCreateWithFlags(&sc, hipStreamNonBlocking);
+    for (size_t S : sizes) {
+        const size_t lines = S / 128;
+        std::vector<unsigned> perm(lines);
+        for (size_t i = 0; i < lines; i++) perm[i] = (unsigned)i;
+        std::mt19937 rng(7);
+        std::shuffle(perm.begin(), perm.end(), rng);
+        std::vector<unsigned> h(S / 4, 0);
+        for (size_t i = 0; i < lines; i++) h[(size_t)perm[i] * 32] = perm[(i + 1) % lines] * 32;   // a cycle over all lines
+        unsigned* buf;
+        hipMalloc(&buf, S);
+        hipMemcpy(buf, h.data(), S, hipMemcpyHostToDevice);
+        const int hops = 20000;
+        hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, sc, buf, perm[0] * 32u, 2000, out, ticks);   // warm
+        hipStreamSynchronize(sc);
+        if (loaded) {
+            *stop = 0;
+            hipLaunchKernelGGL(k_load, dim3(2048), dim3(256), 0, sl, lbuf, ln, stop, out + 1);
+        }
+        hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, sc, buf, perm[12345 % lines] * 32u, hops, out, ticks);
+        hipStreamSynchronize(sc);
+        if (loaded) { *stop = 1; hipStreamSynchronize(sl); }
+        unsigned long long t[2];
+        hipMemcpy(t, ticks, 16, hipMemcpyDeviceToHost);
+        printf("%s buffer %7zu KiB: %7.1f ns per dependent gather (%6.0f cycles)\n", loaded ? "loaded" : "idle  ",
+               S >> 10, t[0] * 10.0 / hops, (double)t[1] / hops);
+        hipFree(buf);
+    }
+    return 0;
+}
