@@ -6,7 +6,7 @@
 #   tools/measure.sh bench NAME:ARGS ...           bench lines (ARGS with _ for spaces, e.g.
 #                                                  c4_P1:--config_c4_--pose_P1)  -> gpurun_out/<TAG>_bench_NAME.json
 #   tools/measure.sh pmc CFG:POSE:KERNEL:FPL:LOOP  PMC passes (FETCH_SIZE, WRITE_SIZE, then TA/TD/TCP/SQ) of the
-#                                                  same bench loop; tools/pmc_summary.py -> profiles/traffic_*.json
+#                                                  same bench loop; tools/pmc_summary.py -> gpurun_out/traffic_*.json (copy to profiles/)
 #   tools/measure.sh prof [NAME:ARGS ...]          rocprofv3 --kernel-trace --stats of bench lines
 #                                                  (default: the driver's bench and the drop-in loop)
 #                                                  -> gpurun_out/<TAG>_prof_NAME/
@@ -70,7 +70,7 @@ pmc)
                 echo "FAILED pmc $t $first"; tail -3 "gpurun_out/${TAG}_pmc_${t}_$first.log"; exit 3; }
         done
         python3 tools/pmc_summary.py --prefix "${TAG}${t}_" --config "$c$suf" --kernel "$kern" --fpl "$fpl" --grid -1 \
-            --out "gpurun_out/traffic_$c$suf.json" && cp "gpurun_out/traffic_$c$suf.json" "profiles/traffic_$c$suf.json"
+            --out "gpurun_out/traffic_$c$suf.json"   # copy into profiles/ from the merged gpurun_out/
     done ;;
 prof)
     [ $# -eq 0 ] && set -- "c4:--steps_20_--warmup_5" "dc_c4:--loop_drawcuda_--steps_20_--warmup_5"
