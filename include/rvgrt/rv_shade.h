@@ -52,13 +52,41 @@
 
 namespace rv {
 
+#ifndef RV_REFL_DIAG   // diagnostics builds: the reflection rays' step counts per wave in STATS frames
+#define RV_REFL_DIAG 0
+#endif
+#if RV_REFL_DIAG
+// [0] lanes, [1] waves, [2] sum of lane steps (sphere + DDA), [3] sum over waves of the wave's longest,
+// [4 + b] sum over waves of min(longest, B), [8 + b] sum over lanes of max(steps - B, 0), B = 16 << b
+static __device__ unsigned long long rv_refl_diag_buf[12];
+__device__ inline void refl_diag_add(uint32_t n) {
+    uint64_t m = __ballot(1);
+    const int first = __builtin_ctzll(m);
+    unsigned long long v[12] = {};
+    while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)n, l);
+        v[0] += 1; v[2] += x; v[3] = v[3] > x ? v[3] : x;
+        for (int b = 0; b < 4; b++) v[8 + b] += x > (16u << b) ? x - (16u << b) : 0u;
+    }
+    v[1] = 1;
+    for (int b = 0; b < 4; b++) v[4 + b] = v[3] < (16u << b) ? v[3] : (16u << b);
+    if ((int)(threadIdx.x & 63u) == first)
+        for (int i = 0; i < 12; i++) atomicAdd(&rv_refl_diag_buf[i], v[i]);
+}
+#endif
+
 // one half-res pixel of distApproximationKernel (StateRender.cu:255-286): its distance (d - 8, the
 // value stored) and shadow texels
 // G: the traversal's DDA look-ahead (every G gives the same hit: rv_device.h trace)
 struct NoPublish { __device__ void operator()(float) const {} };
 // on_dist(d - 8): called once the camera ray is done, before the shadow ray (the flow launch publishes the
 // distance there: the two-phase hand-off, rv_kernels.hip flow_pre_part)
-template <bool STATS, class WV = World, int G = RV_G_PREPASS, class PUB = NoPublish>
+#ifndef RV_SPEC_PP   // the pre-pass rays' speculative sphere steps (rv_device.h trace SPEC: 0, 1 or 3)
+#define RV_SPEC_PP 0
+#endif
+template <bool STATS, class WV = World, int G = RV_G_PREPASS, class PUB = NoPublish, int SPEC = RV_SPEC_PP>
 __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, int ix, int iy,
                                              uint32_t (&c)[NCNT], float& dist_out, float& shadow_out,
                                              const PUB& on_dist = PUB()) {
@@ -67,7 +95,7 @@ __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, 
     f3 dir = ray_dir(f, x, y);
     StepCount sc{};
     RV_GD_KIND(gd::PP_PRIMARY);
-    Hit h = trace<STATS, G, false, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && (G > 1) && RV_DDA_REWALK>(
+    Hit h = trace<STATS, G, false, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && (G > 1) && RV_DDA_REWALK, SPEC>(
         w, f.pos, dir, 0.0f, sc);
     float d = h.hit ? length(sub(h.pos, f.pos)) : 300.0f;
     float s = 1.0f;
@@ -75,7 +103,8 @@ __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, 
     if (STATS) { c[CNT_TRACES]++; c[CNT_PP_PRIMARY]++; c[CNT_UNDEF] += h.undef; }
     if (h.hit && !(RV_ABLATE & 1024)) {
         RV_GD_KIND(gd::PP_SHADOW);
-        Hit sh = trace_sun<STATS, G, false>(w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
+        Hit sh = trace_sun<STATS, G, false, WV, (RV_COL_SUN != 0) && (G > 1) && (RV_DDA_REWALK != 0), SPEC>(
+            w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
         s = sh.hit ? SHADOW_HIT : 1.0f;
         if (STATS) { c[CNT_TRACES]++; c[CNT_PP_SHADOW]++; }
     }
@@ -191,7 +220,13 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         else {
             constexpr int GG = RV_G_REFL ? RV_G_REFL : G;
             constexpr bool COLR = RV_COL_REFL && (GG > 1) && RV_DDA_REWALK && GR == 0 && COLOK;   // throughput launches
+#if RV_REFL_DIAG
+            const uint32_t s0 = sc.sphere + sc.dda;
+#endif
             rh = trace<STATS, GG, RE, (RV_DDA_REWALK != 0), false, WV, COLR>(w, hit.pos, rdir, hround(0.001f), sc);
+#if RV_REFL_DIAG
+            if (STATS) refl_diag_add(sc.sphere + sc.dda - s0);
+#endif
         }
         if (STATS) { c[CNT_TRACES]++; c[CNT_REFL]++; }
         f3 rc;

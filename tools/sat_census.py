@@ -54,10 +54,13 @@ class Replay:
         st = [int(d[k] > 0) - int(d[k] < 0) for k in range(3)]
         YL = min(Y, self.ytop) if st[1] >= 0 else Y
         mx = max(abs(float(v)) for v in d)
-        rec = {"sphere": 0, "sat": 0, "rounds_plain": 0, "rounds_skip": 0, "dda_rounds": 0, "dda": 0}
+        rec = {"sphere": 0, "sat": 0, "rounds_plain": 0, "rounds_skip": 0, "dda_rounds": 0, "dda": 0,
+               "dseq": []}   # dseq: per sphere march, the CSDF bytes its steps read (tools/spec_census.py)
         free = 0
         for _major in range(5):
             oob = False
+            seq = []
+            rec["dseq"].append(seq)
             for _it in range(100):
                 fx, fy, fz = (int(math.floor(float(v))) for v in cur)
                 oob = not (0 <= fx < X and 0 <= fy < YL and 0 <= fz < Z)
@@ -67,6 +70,7 @@ class Replay:
                     break
                 cx, cy, cz = fx >> 1, fy >> 1, fz >> 1
                 dv = int(self.csdf[cz, cy, cx])
+                seq.append(dv)
                 rec["sphere"] += 1
                 rec["rounds_plain"] += 1
                 if free > 0:
@@ -120,9 +124,9 @@ class Replay:
         return rec
 
 
-def main():
-    cfg_name = sys.argv[1] if len(sys.argv) > 1 else "c4"
-    pose = sys.argv[2] if len(sys.argv) > 2 else "P0"
+def setup(cfg_name, pose):
+    """The oracle world, the config's pre-pass rays traced on the host, and the replay (shared with
+    tools/spec_census.py)."""
     from scipy import ndimage
     from oracle import oracle as O
     from rvgrt_amd.configs import CONFIGS, pose_f32
@@ -223,6 +227,17 @@ def main():
     rp = Replay(cs, rad, (N, N, N), int(ytop.value), hz, G)
     hit_index = np.full(n, -1, np.int64)
     hit_index[np.flatnonzero(hit)] = np.arange(m)
+    return dict(rp=rp, solid=solid, org=org, d=d, lanes=lanes, sample=sample, hc=hc, hs=hs, hit=hit, o2=o2,
+                hit_index=hit_index, sun=sun, d1=d1, d2=d2, cs=cs, rad=rad, ytop=ytop, G=G)
+
+
+def main():
+    cfg_name = sys.argv[1] if len(sys.argv) > 1 else "c4"
+    pose = sys.argv[2] if len(sys.argv) > 2 else "P0"
+    e = setup(cfg_name, pose)
+    rp, solid, org, d, lanes, sample = e["rp"], e["solid"], e["org"], e["d"], e["lanes"], e["sample"]
+    hc, hs, hit, o2, hit_index, sun, d1, d2 = (e[k] for k in ("hc", "hs", "hit", "o2", "hit_index", "sun", "d1", "d2"))
+    cs, rad, ytop, G = e["cs"], e["rad"], e["ytop"], e["G"]
 
     def census(idx):
         agg = {k: {"sphere": 0, "sat": 0, "rounds_plain": 0, "rounds_skip": 0} for k in ("camera", "shadow")}

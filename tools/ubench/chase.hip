@@ -2,7 +2,9 @@
 // lone ray's chain (a sphere step's next address is its gather's result).  One lane chases a random
 // cyclic permutation of 128-B lines over a buffer of S bytes (S from L2-resident to far beyond the
 // 256 MB Infinity Cache), optionally while every other CU streams through a separate buffer (the load
-// the tail of a frame launch runs under).  Prints ns per hop.  Not part of the product.
+// the tail of a frame launch runs under).  Mode 2: the same load kept off the chasing lane's CU (CU-masked
+// streams), to split the load's cost into the CU's own memory pipeline and the shared L2 / fabric.
+// Prints ns per hop.  Not part of the product.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -34,7 +36,8 @@ __global__ void k_load(const unsigned* __restrict__ buf, size_t n, volatile unsi
 }
 
 int main(int argc, char** argv) {
-    const bool loaded = argc > 1 && atoi(argv[1]) != 0;
+    const int mode = argc > 1 ? atoi(argv[1]) : 0;
+    const bool loaded = mode != 0;
     const size_t sizes[] = {1u << 20, 4u << 20, 16u << 20, 64u << 20, 128u << 20, 256u << 20, 1024u << 20};
     unsigned *out, *stop, *lbuf = nullptr;
     unsigned long long* ticks;
@@ -44,8 +47,20 @@ int main(int argc, char** argv) {
     const size_t ln = (size_t)512 << 20;   // 2 GiB background buffer
     if (loaded) { hipMalloc(&lbuf, ln * 4); hipMemset(lbuf, 1, ln * 4); }
     hipStream_t sl, sc;
-    hipStreamCreateWithFlags(&sl, hipStreamNonBlocking);
-    hipStreamCreateWithFlags(&sc, hipStreamNonBlocking);
+    if (mode == 2) {
+        hipDeviceProp_t prop;
+        hipGetDeviceProperties(&prop, 0);
+        const int ncu = prop.multiProcessorCount, words = (ncu + 31) / 32;
+        std::vector<uint32_t> mc(words, 0u), ml(words, 0u);
+        mc[0] = 1u;   // the chaser: CU 0
+        for (int i = 1; i < ncu; i++) ml[i / 32] |= 1u << (i % 32);   // the load: every other CU
+        hipExtStreamCreateWithCUMask(&sc, (uint32_t)words, mc.data());
+        hipExtStreamCreateWithCUMask(&sl, (uint32_t)words, ml.data());
+        printf("mode 2: %d CUs, chaser on CU 0, load on the other %d\n", ncu, ncu - 1);
+    } else {
+        hipStreamCreateWithFlags(&sl, hipStreamNonBlocking);
+        hipStreamCreateWithFlags(&sc, hipStreamNonBlocking);
+    }
     for (size_t S : sizes) {
         const size_t lines = S / 128;
         std::vector<unsigned> perm(lines);
@@ -69,7 +84,7 @@ int main(int argc, char** argv) {
         if (loaded) { *stop = 1; hipStreamSynchronize(sl); }
         unsigned long long t[2];
         hipMemcpy(t, ticks, 16, hipMemcpyDeviceToHost);
-        printf("%s buffer %7zu KiB: %7.1f ns per dependent gather (%6.0f cycles)\n", loaded ? "loaded" : "idle  ",
+        printf("%s buffer %7zu KiB: %7.1f ns per dependent gather (%6.0f cycles)\n", mode == 2 ? "isolat" : loaded ? "loaded" : "idle  ",
                S >> 10, t[0] * 10.0 / hops, (double)t[1] / hops);
         hipFree(buf);
     }
