@@ -694,6 +694,7 @@ def main():
             "dropin": dropin,
             "cpu_baseline": cpu,
             "world_build_s": round(world_s, 3),
+            "tex_table_bytes": int(r.tex_table_info()[1]),
             "stats": st_all,
         }
         print(json.dumps(line), flush=True)

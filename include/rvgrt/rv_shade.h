@@ -212,6 +212,7 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         // timing ablations: 2048 the wave normal's two fbm3D, 8192 the reflection ray, 4096 its shadow ray
         float nxw = (RV_ABLATE & 2048) ? 0.0f : fbm3D(hit.pos.x, hit.pos.z, f.time, 3, 0.06f, 2.0f, 0.6f);
         float nyw = (RV_ABLATE & 2048) ? 0.0f : fbm3D(hit.pos.z, hit.pos.x, f.time + 112.0f, 3, 0.06f, 2.0f, 0.6f);
+        if (RV_ABLATE & 16384) { nxw = nxw * 0.0f; nyw = nyw * 0.0f; }   // timing: the noise computed, not used
         f3 dn = normalize(add(hit.normal, V(nxw * 0.1f, nyw * 0.1f, 0.0f)));
         f3 rdir = reflect(dir, dn);
         RV_GD_KIND(gd::REFL);

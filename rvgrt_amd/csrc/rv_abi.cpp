@@ -344,7 +344,7 @@ rv_status rv_set_pipeline(rv_ctx* c, int32_t on) {
 rv_status rv_tex_table_info(rv_ctx* c, int32_t* active, uint64_t* bytes) {
     if (!c) return RV_ERR_INVALID;
     if (active) *active = c->tex != nullptr;
-    if (bytes) *bytes = c->tex ? (uint64_t)c->w.X * c->w.Y * c->w.Z * 4 : 0;
+    if (bytes) *bytes = c->tex ? (uint64_t)c->w.X * c->w.tex_ny * c->w.Z * 4 : 0;
     return RV_OK;
 }
 
@@ -397,9 +397,10 @@ rv_status rv_sync(rv_ctx* c) {
     return RV_OK;
 }
 
-// sampleTexture's tile table (World::tex, rv_device.h tex_index): 4 B per voxel, a function of the voxel
-// coordinates only, so it is built once, at the first world build or import (bench.py's world_build_s
-// includes it) and kept through rebuilds.  It is optional -- a context without it evaluates the noise in
+// sampleTexture's tile table (World::tex, rv_device.h tex_index): 4 B per voxel of the rows below the sky
+// exit (World::ytop rounded up to 8), a function of the voxel coordinates only, so it is built once, after
+// the first world build or bits import (bench.py's world_build_s includes it) and kept through rebuilds (a
+// hit above its rows takes the noise).  It is optional -- a context without it evaluates the noise in
 // the kernels, with identical tiles -- so it is only allocated when it leaves room: the memory this
 // context may still allocate (CSDF build scratch, the GI scratch grid, two grouped-frame sets of 32
 // frames, the pipelined loop's buffers) plus 1 GiB, and at most half the device's free memory (other
@@ -410,7 +411,8 @@ static rv_status tex_table(rv_ctx* c) {
     const char* te = getenv("RV_TEX_TABLE");
     if (te && te[0] == '0') return RV_OK;
     const bool force = te && te[0] == '1';
-    const size_t tb = (size_t)c->w.X * c->w.Y * c->w.Z * 4;
+    const uint32_t ny = std::min((uint32_t)c->w.Y, (c->w.ytop + 7u) & ~7u);
+    const size_t tb = (size_t)c->w.X * ny * c->w.Z * 4;
     if (!force) {
         size_t fr = 0, total = 0;
         HIP_TRY(c, hipMemGetInfo(&fr, &total));
@@ -424,6 +426,7 @@ static rv_status tex_table(rv_ctx* c) {
         (void)hipGetLastError();
         return RV_OK;
     }
+    c->w.tex_ny = ny;
     launch_tex_table(c->stream, c->tex, c->w);
     LAUNCH_CHECK(c);
     c->w.tex = c->tex;
@@ -504,10 +507,10 @@ rv_status rv_world_build(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
     c->geom_ver++;
-    if (rv_status ts = tex_table(c)) return ts;
     launch_fill_bricks(c->stream, c->brick, current_world(c), c->cfg.seed_x, c->cfg.seed_z);
     LAUNCH_CHECK(c);
     if (rv_status ts = world_top(c)) return ts;
+    if (rv_status ts = tex_table(c)) return ts;
     rv_status s = rv_csdf_build(c);
     if (s != RV_OK) return s;
     s = rv_gi_init(c);
@@ -520,7 +523,6 @@ rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t byte
     if (!c || !host) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
     if (kind != RV_WORLD_GI) c->geom_ver++;
-    if (rv_status ts = tex_table(c)) return ts;
     if (kind == RV_WORLD_BITS) {
         if (bytes != n_bits_words(c) * 4) return fail(c, RV_ERR_INVALID, "bits size mismatch");
         uint32_t* d = nullptr;
@@ -531,6 +533,7 @@ rv_status rv_world_import(rv_ctx* c, int32_t kind, const void* host, size_t byte
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         hipFree(d);
         if (rv_status ts = world_top(c)) return ts;
+        if (rv_status ts = tex_table(c)) return ts;
     } else if (kind == RV_WORLD_CSDF) {
         if (bytes != n_csdf(c)) return fail(c, RV_ERR_INVALID, "csdf size mismatch");
         uint8_t* d = nullptr;

@@ -153,14 +153,23 @@ void rvh_simplex3D(const float* xyz, float* out, int64_t n) {
 
 // sampleTexture's tile (0xYX) for n positions in a 2^lx x 2^ly x 2^lz world, through the World::tex
 // table (built on the host with k_tex_table's element function) and through the noise (tex = null)
-void rvh_texture_tiles(int lx, int ly, int lz, const float* pos, int64_t n, int32_t* via_table, int32_t* via_noise) {
+// ny: the rows the table covers (0: all; else a multiple of 8, the band below the sky exit)
+void rvh_texture_tiles(int lx, int ly, int lz, int ny, const float* pos, int64_t n, int32_t* via_table,
+                       int32_t* via_noise) {
     World w{};
     w.X = 1 << lx; w.Y = 1 << ly; w.Z = 1 << lz;
-    w.lbz = lz - 3; w.lbzy = (lz - 3) + (ly - 3);
-    std::vector<uint32_t> tex((size_t)w.X * w.Y * w.Z);
+    w.lbx = lx - 3; w.lbz = lz - 3; w.lbzy = (lz - 3) + (ly - 3);
+    w.tex_ny = ny ? (uint32_t)ny : (uint32_t)w.Y;
+    std::vector<uint32_t> tex((size_t)w.X * w.tex_ny * w.Z, 0xFFFFFFFFu);
     for (uint32_t z = 0; z < (uint32_t)w.Z; z++)
-        for (uint32_t y = 0; y < (uint32_t)w.Y; y++)
+        for (uint32_t y = 0; y < w.tex_ny; y++)
             for (uint32_t x = 0; x < (uint32_t)w.X; x++) tex[tex_index(w, x, y, z)] = tex_table_entry(x, y, z);
+    for (size_t i = 0; i < tex.size(); i++) {   // every entry written once, by k_tex_table's order too
+        uint32_t bx, by, bz;
+        tex_brick_coords(w, i >> 9, bx, by, bz);
+        const uint32_t l = (uint32_t)i & 511u;
+        if (tex[i] != tex_table_entry(bx * 8u + ((l >> 3) & 7u), by * 8u + (l >> 6), bz * 8u + (l & 7u))) return;
+    }
     World wn = w;
     w.tex = tex.data();
     for (int64_t i = 0; i < n; i++) {

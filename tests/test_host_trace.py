@@ -95,8 +95,8 @@ def test_simplex3d_equals_oracle(host_lib):
 
 
 def test_texture_tile_table_equals_noise(host_lib):
-    """World::tex (rv_device.h tex_index / tex_table_entry, built once per context by k_tex_table)
-    gives the atlas tile sampleTexture's noise picks (src/raytracing_functions.cu:41-54) for every
+    """World::tex (rv_device.h tex_index / tex_table_entry, built once per context by k_tex_table over
+    the rows below the sky exit) gives the atlas tile sampleTexture's noise picks (src/raytracing_functions.cu:41-54) for every
     hit position: lattice points, faces (integral coordinates), the carry boundaries of the +121.3 /
     +1321.3 / +721.5 offsets (fractions near 0.7 and 0.5), the world's far faces and outside
     positions (the kernels then evaluate the noise)."""
@@ -117,13 +117,13 @@ def test_texture_tile_table_equals_noise(host_lib):
     p[5 * k + 500:5 * k + 1000] = dims + rng.uniform(0, 3, (500, 3))  # outside: noise path
     p[5 * k + 1000:5 * k + 1500] = -rng.uniform(0, 3, (500, 3))
     pts = np.ascontiguousarray(p.astype(np.float32))
-    tab = np.empty(n, np.int32)
-    noi = np.empty(n, np.int32)
-    host_lib.rvh_texture_tiles.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
-                                           C.c_void_p]
-    host_lib.rvh_texture_tiles(lx, ly, lz, pts.ctypes.data, n, tab.ctypes.data, noi.ctypes.data)
-    assert np.array_equal(tab, noi)
-    assert len(np.unique(noi)) >= 3                                 # several tiles exercised
+    host_lib.rvh_texture_tiles.argtypes = [C.c_int] * 4 + [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+    for ny in (0, 8):   # the whole world; a band of the lowest 8 rows (the rest: noise)
+        tab = np.full(n, -1, np.int32)
+        noi = np.full(n, -2, np.int32)
+        host_lib.rvh_texture_tiles(lx, ly, lz, ny, pts.ctypes.data, n, tab.ctypes.data, noi.ctypes.data)
+        assert np.array_equal(tab, noi), ny
+        assert len(np.unique(noi)) >= 3                             # several tiles exercised
 
 
 @pytest.mark.parametrize("variant", ["g1", "g4", "g8", "g4_replay"])

@@ -7,7 +7,9 @@ RVGRT_LIB=rvgrt_amd/variants/diag/librvgrt_hip.so); the context records its last
 (env RV_FLOW_WAVE_TRACE) and dumps them at rv_destroy.  Prints, per part, when its waves start and end
 (us from the first wave's start), their lifetimes, the render waves' wait for their pre-pass tiles, and
 the critical path: the last render waves to finish -- when they started, how long they waited, how long
-they ran.  Not part of the product.
+they ran; and the pre-pass tiles of the longest waves, with the RV_FLOW_OPTS value that runs that tile's
+wave alone (4: no GI or render part, 8: one pre-pass tile) -- its chain on an idle chip.  Not part of
+the product.
 
 usage: python tools/flow_waves.py [config] [pose] [frames]
 """
@@ -61,7 +63,8 @@ def main():
     start = (rec[:, 1] - t0) / 100.0        # 10-ns ticks -> us
     wait = (rec[:, 2] - t0) / 100.0
     end = (rec[:, 3] - t0) / 100.0
-    part = rec[:, 0]
+    part = rec[:, 0] & 0xFF
+    tile = rec[:, 0] >> 8                   # pre-pass waves: bx | by << 12 (diagnostics builds)
     names = {1: "prepass", 0: "gi", 2: "render"}
     print(f"{cfg.name} {pose}: {W}x{H}, workgroups pre-pass {lens[0]}, GI {lens[1]}, render {lens[2]}; "
           f"launch span {end.max():.1f} us")
@@ -82,6 +85,10 @@ def main():
     for i in idx:
         print(f"    start {start[i]:7.1f}  ready {wait[i]:7.1f}  end {end[i]:7.1f}  run {end[i] - wait[i]:7.1f}")
     pp = part == 1
+    top = np.flatnonzero(pp)[np.argsort(-(end[pp] - start[pp]))][:5]
+    print("  longest pre-pass waves (tile bx, by: life us): " +
+          ", ".join(f"{tile[i] & 0xFFF},{tile[i] >> 12}: {end[i] - start[i]:.1f}" for i in top))
+    print(f"  LONGEST_TILE_OPTS {int((tile[top[0]] << 8) | 8 | 4)}")
     print(f"  pre-pass done at {end[pp].max():.1f} us; GI done at {end[part == 0].max() if (part == 0).any() else 0:.1f} us; "
           f"render waves dispatched from {start[m].min():.1f} us to {start[m].max():.1f} us")
 

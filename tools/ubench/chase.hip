@@ -4,7 +4,8 @@
 // 256 MB Infinity Cache), optionally while every other CU streams through a separate buffer (the load
 // the tail of a frame launch runs under).  Mode 2: the same load kept off the chasing lane's CU (CU-masked
 // streams), to split the load's cost into the CU's own memory pipeline and the shared L2 / fabric.
-// Prints ns per hop.  Not part of the product.
+// Argument 2: lanes of the chasing wave (each its own stretch of the cycle: a wave-wide divergent gather
+// per hop, as a sphere step of a full wave).  Prints ns per hop.  Not part of the product.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -12,18 +13,20 @@
 #include <random>
 #include <algorithm>
 
-__global__ void k_chase(const unsigned* __restrict__ buf, unsigned start, int hops, unsigned* out,
-                        unsigned long long* ticks) {
-    if (threadIdx.x != 0) return;
-    unsigned p = start;
+__global__ void k_chase(const unsigned* __restrict__ buf, const unsigned* __restrict__ starts, int hops, unsigned* out,
+                        unsigned long long* ticks, int lanes) {
+    if ((int)threadIdx.x >= lanes) return;
+    unsigned p = starts[threadIdx.x];   // lane l: lines / lanes further along the cycle (disjoint stretches)
     const unsigned long long t0 = __builtin_readcyclecounter();
     const unsigned long long r0 = wall_clock64();
     for (int i = 0; i < hops; i++) p = buf[p];
     const unsigned long long r1 = wall_clock64();
     const unsigned long long t1 = __builtin_readcyclecounter();
-    out[0] = p;
-    ticks[0] = r1 - r0;
-    ticks[1] = t1 - t0;
+    if (threadIdx.x == 0) {
+        out[0] = p;
+        ticks[0] = r1 - r0;
+        ticks[1] = t1 - t0;
+    } else if (p == 0xFFFFFFFFu) out[1] = p;
 }
 
 // background load: each wave streams a private slice (coalesced dword loads), until *stop is set
@@ -37,6 +40,7 @@ __global__ void k_load(const unsigned* __restrict__ buf, size_t n, volatile unsi
 
 int main(int argc, char** argv) {
     const int mode = argc > 1 ? atoi(argv[1]) : 0;
+    const int lanes = argc > 2 ? atoi(argv[2]) : 1;   // lanes of the chasing wave, each on its own stretch
     const bool loaded = mode != 0;
     const size_t sizes[] = {1u << 20, 4u << 20, 16u << 20, 64u << 20, 128u << 20, 256u << 20, 1024u << 20};
     unsigned *out, *stop, *lbuf = nullptr;
@@ -73,20 +77,25 @@ int main(int argc, char** argv) {
         hipMalloc(&buf, S);
         hipMemcpy(buf, h.data(), S, hipMemcpyHostToDevice);
         const int hops = 20000;
-        hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, sc, buf, perm[0] * 32u, 2000, out, ticks);   // warm
+        unsigned hst[64], *dst;
+        for (int l = 0; l < 64; l++) hst[l] = perm[(12345 + (size_t)l * (lines / 64)) % lines] * 32u;
+        hipMalloc(&dst, sizeof hst);
+        hipMemcpy(dst, hst, sizeof hst, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, sc, buf, dst, 2000, out, ticks, 1);   // warm
         hipStreamSynchronize(sc);
         if (loaded) {
             *stop = 0;
             hipLaunchKernelGGL(k_load, dim3(2048), dim3(256), 0, sl, lbuf, ln, stop, out + 1);
         }
-        hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, sc, buf, perm[12345 % lines] * 32u, hops, out, ticks);
+        hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, sc, buf, dst, hops, out, ticks, lanes);
         hipStreamSynchronize(sc);
         if (loaded) { *stop = 1; hipStreamSynchronize(sl); }
         unsigned long long t[2];
         hipMemcpy(t, ticks, 16, hipMemcpyDeviceToHost);
-        printf("%s buffer %7zu KiB: %7.1f ns per dependent gather (%6.0f cycles)\n", mode == 2 ? "isolat" : loaded ? "loaded" : "idle  ",
-               S >> 10, t[0] * 10.0 / hops, (double)t[1] / hops);
+        printf("%s %2d lanes, buffer %7zu KiB: %7.1f ns per dependent gather (%6.0f cycles)\n",
+               mode == 2 ? "isolat" : loaded ? "loaded" : "idle  ", lanes, S >> 10, t[0] * 10.0 / hops, (double)t[1] / hops);
         hipFree(buf);
+        hipFree(dst);
     }
     return 0;
 }
