@@ -811,9 +811,9 @@ RV_HIDDEN rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles, int which) 
                                    ((uint32_t)f.ntiles + 7u) & ~7u);
             } else {
                 if (pre) launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS],
-                                            n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh));
+                                            n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh), chunks_x(f.hw));
                 launch_chunk_order(c->stream, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER],
-                                   n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H));
+                                   n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H), chunks_x(f.W));
             }
             LAUNCH_CHECK(c);
         }
@@ -972,9 +972,9 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
         c->frames_since_order = 0;
         launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                           n_chunks_pad(f.hw, f.hh));
+                           n_chunks_pad(f.hw, f.hh), chunks_x(f.hw));
         launch_chunk_order(c->stream, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
-                           n_chunks_pad(f.W, f.H));
+                           n_chunks_pad(f.W, f.H), chunks_x(f.W));
         LAUNCH_CHECK(c);
     }
     return RV_OK;

@@ -363,9 +363,9 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
                 launch_chunk_order(S, c->tile_cost, c->tile_order, (uint32_t)f.ntiles, ((uint32_t)f.ntiles + 7u) & ~7u);
             } else {
                 launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                                   n_chunks_pad(f.hw, f.hh));
+                                   n_chunks_pad(f.hw, f.hh), chunks_x(f.hw));
                 launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
-                                   n_chunks_pad(f.W, f.H));
+                                   n_chunks_pad(f.W, f.H), chunks_x(f.W));
             }
             LAUNCH_CHECK(c);
         }
@@ -641,9 +641,9 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
                 launch_chunk_order(S, c->tile_cost, c->tile_order, nt, (nt + 7u) & ~7u);
             } else {
                 launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(fo.hw, fo.hh),
-                                   n_chunks_pad(fo.hw, fo.hh));
+                                   n_chunks_pad(fo.hw, fo.hh), chunks_x(fo.hw));
                 launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(W, H),
-                                   n_chunks_pad(W, H));
+                                   n_chunks_pad(W, H), chunks_x(W));
             }
             LAUNCH_CHECK(c);
         }
