@@ -620,8 +620,8 @@ static rv_status gi_update(rv_ctx* c, uint32_t frame, uint64_t first, uint64_t c
         std::swap(c->gi, c->gi_tmp);   // full sweep: flip the double buffer
         c->gi_swapped_at = c->frame_seq;
     } else {
-        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice,
-                                  c->stream));
+        launch_copy_u32(c->stream, c->gi + first, c->gi_tmp + first, count);
+        LAUNCH_CHECK(c);
     }
     return mark_world(c);
 }
@@ -647,8 +647,8 @@ rv_status rv_update_gi_data(rv_ctx* c) {
         if (c->spec_stream != c->stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_spec, 0));
         if (rv_status ws = wait_all_frames(c)) return ws;
         if (timed) HIP_TRY(c, hipEventRecord(e[NSTAGE], c->stream));
-        HIP_TRY(c, hipMemcpyAsync(c->gi + c->gi_offset, c->gi_tmp + c->gi_offset, count * 4, hipMemcpyDeviceToDevice,
-                                  c->stream));
+        launch_copy_u32(c->stream, c->gi + c->gi_offset, c->gi_tmp + c->gi_offset, count);
+        LAUNCH_CHECK(c);
         if (timed) HIP_TRY(c, hipEventRecord(e[NSTAGE + 1], c->stream));
         s = mark_world(c);
     } else {
@@ -803,17 +803,17 @@ RV_HIDDEN rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles, int which) 
         }
         // SCHED_COST: re-order the chunks by the wave lifetimes (max over
         // the frames since the last ordering) every order_every frames; a
-        // kernel boundary costs ~6 us, the ordering itself ~4 us.
+        // kernel boundary costs ~6 us, the ordering itself ~4 us (both grids' orderings in one launch).
         if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
             c->frames_since_order = 0;
             if (tiles) {
                 launch_chunk_order(c->stream, c->tile_cost, c->tile_order, (uint32_t)f.ntiles,
                                    ((uint32_t)f.ntiles + 7u) & ~7u);
             } else {
-                if (pre) launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS],
-                                            n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh), chunks_x(f.hw));
-                launch_chunk_order(c->stream, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER],
-                                   n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H), chunks_x(f.W));
+                launch_chunk_order(c->stream, pre ? c->chunk_cost[CG_PREPASS] : nullptr, c->chunk_order[CG_PREPASS],
+                                   n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh), chunks_x(f.hw),
+                                   c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
+                                   n_chunks_pad(f.W, f.H), chunks_x(f.W));
             }
             LAUNCH_CHECK(c);
         }
@@ -972,9 +972,8 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
         c->frames_since_order = 0;
         launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                           n_chunks_pad(f.hw, f.hh), chunks_x(f.hw));
-        launch_chunk_order(c->stream, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
-                           n_chunks_pad(f.W, f.H), chunks_x(f.W));
+                           n_chunks_pad(f.hw, f.hh), chunks_x(f.hw), c->chunk_cost[CG_RENDER],
+                           c->chunk_order[CG_RENDER], n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H), chunks_x(f.W));
         LAUNCH_CHECK(c);
     }
     return RV_OK;

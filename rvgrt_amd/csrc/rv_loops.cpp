@@ -219,15 +219,18 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
     if (!use_gi) {
         launch_gi_update(S, c->gi, c->gi_tmp, w, sun_dir(), fr, first, count, cnt_gi, c->gi_stats);
         LAUNCH_CHECK(c);
-        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+        launch_copy_u32(S, c->gi + first, c->gi_tmp + first, count);
+        LAUNCH_CHECK(c);
     } else if (xchg) {   // ... or kept from the previous call: this rank's share, exchanged now
         if (rv_status as = comm_all_gather(c, comm, c->pipe_gi_stage, c->pipe_gi_all, chunk * 4, c->comm_stream))
             return as;
         HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
         HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[1], 0));
-        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->pipe_gi_all, count * 4, hipMemcpyDeviceToDevice, S));
+        launch_copy_u32(S, c->gi + first, c->pipe_gi_all, count);
+        LAUNCH_CHECK(c);
     } else if (!probe) {
-        HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+        launch_copy_u32(S, c->gi + first, c->gi_tmp + first, count);
+        LAUNCH_CHECK(c);
     }
     if (!use_pp) {
         FrameParams f = make_params_d(c, q.at(0), flags);
@@ -320,7 +323,8 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
                     return as;
                 HIP_TRY(c, hipEventRecord(c->pipe_ev[1], c->comm_stream));
                 HIP_TRY(c, hipStreamWaitEvent(S, c->pipe_ev[1], 0));
-                HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->pipe_gi_all, count * 4, hipMemcpyDeviceToDevice, S));
+                launch_copy_u32(S, c->gi + first, c->pipe_gi_all, count);
+        LAUNCH_CHECK(c);
             }
             // frame k's packed tiles to rank 0, after the all-gather on the comm stream
             if (root)
@@ -341,7 +345,8 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
                 if (rv_status us = untile(k - 1)) return us;
         } else {
             if (apply && !probe)
-                HIP_TRY(c, hipMemcpyAsync(c->gi + first, c->gi_tmp + first, count * 4, hipMemcpyDeviceToDevice, S));
+                launch_copy_u32(S, c->gi + first, c->gi_tmp + first, count);
+        LAUNCH_CHECK(c);
             if (tiles && N == 1) {   // one rank: assemble locally
                 launch_untile(S, c->pipe_tbuf[k & 1], c->untile_ids.d, (int)c->shard_all.size(), T, tiles_x, W, H,
                               c->color, c->color_pitch, c->shard_max, 1, 0, bpp);
@@ -363,9 +368,8 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
                 launch_chunk_order(S, c->tile_cost, c->tile_order, (uint32_t)f.ntiles, ((uint32_t)f.ntiles + 7u) & ~7u);
             } else {
                 launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                                   n_chunks_pad(f.hw, f.hh), chunks_x(f.hw));
-                launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
-                                   n_chunks_pad(f.W, f.H), chunks_x(f.W));
+                                   n_chunks_pad(f.hw, f.hh), chunks_x(f.hw), c->chunk_cost[CG_RENDER],
+                                   c->chunk_order[CG_RENDER], n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H), chunks_x(f.W));
             }
             LAUNCH_CHECK(c);
         }
@@ -641,9 +645,8 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
                 launch_chunk_order(S, c->tile_cost, c->tile_order, nt, (nt + 7u) & ~7u);
             } else {
                 launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(fo.hw, fo.hh),
-                                   n_chunks_pad(fo.hw, fo.hh), chunks_x(fo.hw));
-                launch_chunk_order(S, c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(W, H),
-                                   n_chunks_pad(W, H), chunks_x(W));
+                                   n_chunks_pad(fo.hw, fo.hh), chunks_x(fo.hw), c->chunk_cost[CG_RENDER],
+                                   c->chunk_order[CG_RENDER], n_chunks(W, H), n_chunks_pad(W, H), chunks_x(W));
             }
             LAUNCH_CHECK(c);
         }
