@@ -14,6 +14,14 @@
 #                                                  REPS rounds, ms/frame of each        -> gpurun_out/<TAG>_ab.txt
 #   tools/measure.sh shard CFG GROUP [NS]          slowest rank share per N (tools/shard_probe.py, 64-px tiles,
 #                                                  GI shard, no exchange)               -> gpurun_out/<TAG>_shard.txt
+#   tools/measure.sh shard-orders ORDER ...        C4's slowest 8-rank share at one frame per launch per
+#                                                  RV_PIPE_ORDER (hex digits, lowest ids first: 1 pre-pass,
+#                                                  0 GI, 2 render)                      -> gpurun_out/<TAG>_shard_orders.txt
+#   tools/measure.sh pmc-l1 CFG POSE KERNEL        L1/L2/UTCL1 and TD/TCP stall counters of one bench loop's
+#                                                  kernel (three --pmc passes)          -> gpurun_out/<TAG>_pmc_l1_CFG.txt
+#   tools/measure.sh tile-alone CFG POSE FRAMES    flow-launch timelines (tools/flow_waves.py, the diag build in
+#                                                  rvgrt_amd/variants/diag): whole, pre-pass alone, the longest
+#                                                  pre-pass tile alone                  -> gpurun_out/<TAG>_fw_*.log
 # TAG (env, default r05) prefixes every output; STEPS/WARMUP (env) size the bench runs (default 200/20).
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
@@ -102,6 +110,37 @@ shard)
     SHARD_GROUP=$g SHARD_NS=$ns RV_GI_SHARD_PROBE=1 timeout -k 10 500 python tools/shard_probe.py "$c" 1 64 \
         > "gpurun_out/${TAG}_shard_${c}_$g.log" 2>&1 || { echo "FAILED shard"; tail -5 "gpurun_out/${TAG}_shard_${c}_$g.log"; exit 3; }
     grep -v "frames \.\.\.\|amdgpu.ids" "gpurun_out/${TAG}_shard_${c}_$g.log" | tee -a "gpurun_out/${TAG}_shard.txt" ;;
+shard-orders)
+    out="gpurun_out/${TAG}_shard_orders.txt"
+    for o in "$@"; do
+        echo "== RV_PIPE_ORDER=$o" | tee -a "$out"
+        RV_PIPE_ORDER=$o SHARD_GROUP=0 SHARD_NS=8 RV_GI_SHARD_PROBE=1 timeout -k 10 300 python tools/shard_probe.py c4 1 64 \
+            > "gpurun_out/${TAG}_shard_order_$o.log" 2>&1 || { echo "FAILED shard order $o"; exit 3; }
+        grep -E "whole frame|N=8" "gpurun_out/${TAG}_shard_order_$o.log" | tee -a "$out"
+    done ;;
+pmc-l1)
+    c=$1; pose=${2:-P0}; kern=${3:-k_ref_pipe}; i=0
+    for set in "TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_SERIALIZATION_STALL_sum TD_COALESCABLE_WAVEFRONT_sum TD_LOAD_WAVEFRONT_sum GRBM_GUI_ACTIVE" \
+               "TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TD_TC_STALL_sum TD_SPI_STALL_sum GRBM_GUI_ACTIVE" \
+               "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCP_LATENCY_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+        i=$((i + 1))
+        rm -rf "gpurun_out/l1_${TAG}${c}_$i"
+        echo "== pmc-l1 $c pass $i ($(date +%T))"
+        timeout -s KILL 150 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "gpurun_out/l1_${TAG}${c}_$i" -o run \
+            -- python3 bench.py --config "$c" --pose "$pose" --steps 32 --warmup 8 --cpu-seconds 0 --dropin-leg 0 \
+            > "gpurun_out/${TAG}_l1_${c}_$i.log" 2>&1 || { echo "FAILED pass $i"; tail -3 "gpurun_out/${TAG}_l1_${c}_$i.log"; exit 3; }
+    done
+    python3 tools/pmc_summary.py --l1 "l1_${TAG}${c}_" --kernel "$kern" > "gpurun_out/${TAG}_pmc_l1_$c.txt" || exit 3
+    cat "gpurun_out/${TAG}_pmc_l1_$c.txt" ;;
+tile-alone)
+    c=${1:-c3}; pose=${2:-P0}; n=${3:-40}
+    export RVGRT_LIB=rvgrt_amd/variants/diag/librvgrt_hip.so
+    run fw_full 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    opts=$(grep LONGEST_TILE_OPTS "gpurun_out/${TAG}_fw_full.log" | awk '{print $2}')
+    RV_FLOW_OPTS=4 run fw_alone 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    RV_FLOW_OPTS=$opts run fw_tile 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    grep -h "launch span\|life\|longest pre-pass" "gpurun_out/${TAG}_fw_full.log" "gpurun_out/${TAG}_fw_alone.log" \
+        "gpurun_out/${TAG}_fw_tile.log" ;;
 *)
-    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard ..."; exit 2 ;;
+    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard|shard-orders|pmc-l1|tile-alone ..."; exit 2 ;;
 esac

@@ -31,7 +31,19 @@ def main():
     ap.add_argument("--fpl", type=int, default=8, help="frames per launch of the profiled bench run")
     ap.add_argument("--prefix", default="", help="pass directories pmc_<prefix>* only (tools/measure.sh pmc: TAG + config)")
     ap.add_argument("--grid", type=int, default=0, help="dispatches of this Grid_Size only (-1: the largest, i.e. the full-group launches)")
+    ap.add_argument("--l1", default=None, help="print every counter's per-launch mean of the passes <dir>/<L1>* (measure.sh pmc-l1)")
     a = ap.parse_args()
+    if a.l1:
+        vals = collections.defaultdict(list)
+        for f in glob.glob(os.path.join(a.dir, f"{a.l1}*", "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if a.kernel in row["Kernel_Name"]:
+                    vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        if not vals:
+            raise SystemExit("no counter rows for " + a.kernel)
+        for k in sorted(vals):
+            print(f"{k:40s} {sum(vals[k]) / len(vals[k]):16.0f}  ({len(vals[k])} launches)")
+        return
     vals = collections.defaultdict(list)
     files = glob.glob(os.path.join(a.dir, f"pmc_{a.prefix}*", "*counter_collection.csv"))
     if a.grid < 0:   # the largest grid of the kernel: the full-group launches of a grouped loop
