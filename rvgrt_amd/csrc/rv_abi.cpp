@@ -971,9 +971,9 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     }
     if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
         c->frames_since_order = 0;
-        // a latency-variant flow frame (C3's 1080p) orders each XCD's chunks as one vertical strip of the image
-        // (env RV_FLOW_REGIONS=0: off); whole-frame throughput launches keep the round-robin deal
-        static const int flow_regions = [] { const char* e = getenv("RV_FLOW_REGIONS"); return e ? atoi(e) : 1; }();
+        // env RV_FLOW_REGIONS=1: a latency-variant flow frame (C3's 1080p) orders each XCD's chunks as one vertical
+        // strip of the image -- C3 P0 drop-in -1.1 %, P1 +5 % (profiles/r05/flow_regions_ab.txt): off by default
+        static const int flow_regions = [] { const char* e = getenv("RV_FLOW_REGIONS"); return e ? atoi(e) : 0; }();
         const int regions = flow_regions && pipe_latency_variant(f, p.len[2]) ? 1 : -1;
         launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
                            n_chunks_pad(f.hw, f.hh), chunks_x(f.hw), c->chunk_cost[CG_RENDER],
