@@ -31,7 +31,7 @@ class rv_config(C.Structure):
                 ("seed_x", C.c_int32), ("seed_z", C.c_int32),
                 ("ref_compat", C.c_int32), ("ref_oob_jy", C.c_float),
                 ("atlas_rgba8", C.c_void_p), ("atlas_w", C.c_int32), ("atlas_h", C.c_int32),
-                ("gi_rays_per_frame", C.c_uint32)]
+                ("gi_rays_per_frame", C.c_uint32), ("gi_init_saturate", C.c_int32)]
 
 
 class rv_camera(C.Structure):

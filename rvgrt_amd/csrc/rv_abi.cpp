@@ -496,7 +496,8 @@ rv_status rv_csdf_build(rv_ctx* c) {
 rv_status rv_gi_init(rv_ctx* c) {
     if (!c) return RV_ERR_INVALID;
     if (rv_status ws = wait_all_frames(c)) return ws;
-    launch_gi_init(c->stream, c->gi, current_world(c), sun_dir(), c->counters + ST_GI * NCNT);
+    launch_gi_init(c->stream, c->gi, current_world(c), sun_dir(),
+                   c->cfg.gi_init_saturate ? RV_GI_LIT_SATURATE : RV_GI_LIT_REFERENCE, c->counters + ST_GI * NCNT);
     LAUNCH_CHECK(c);
     c->gi_frame = 0;
     c->gi_offset = 0;

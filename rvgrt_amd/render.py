@@ -139,7 +139,7 @@ class StateRender:
 
     def __init__(self, log2_dims=(9, 9, 9), width=1920, height=1080, flags=_lib.RV_FLAGS_REFERENCE,
                  atlas=None, device=0, seed=(0, 0), ref_compat=True, ref_oob_jy=0.0,
-                 gi_rays_per_frame=0):
+                 gi_rays_per_frame=0, gi_init_saturate=False):
         self._L = _lib.load()
         self.width, self.height = int(width), int(height)
         self.log2_dims = tuple(int(v) for v in log2_dims)
@@ -154,6 +154,7 @@ class StateRender:
             cfg.atlas_rgba8 = self._atlas.ctypes.data
             cfg.atlas_h, cfg.atlas_w = self._atlas.shape[0], self._atlas.shape[1]
         cfg.gi_rays_per_frame = int(gi_rays_per_frame)
+        cfg.gi_init_saturate = int(bool(gi_init_saturate))
         h = C.c_void_p()
         st = self._L.rv_create(C.byref(cfg), int(device), C.byref(h))
         if st != 0:
