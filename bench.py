@@ -31,7 +31,16 @@ Multi-GPU: the frame is split into interleaved screen tiles (rv_set_tile_shard),
 every rank renders its tiles of the same frame against its own locally
 generated replica of the world and 1/N of the GI update's cells (RCCL
 all-gather), and rank 0 gathers the packed tiles over RCCL and assembles the
-frame: strong scaling of a fixed frame.
+frame: strong scaling of a fixed frame.  `--gpus N` is honoured either way:
+under a launcher (torch.distributed.run) WORLD_SIZE must equal N; without one
+(WORLD_SIZE unset, N > 1) this process starts N rank processes of itself
+before touching the GPU and prints rank 0's line.
+
+Loop modes.  `value` is measured in the same loop mode at every N, the one
+N = 1 uses for the config (C4/C5: one pipelined launch per frame; C3: 8-frame
+groups), so a 1 -> 8 curve compares like with like.  For reference frames the
+line also reports the other mode ("modes": per-frame vs grouped 16-frame
+launches), timed on the same context after the main region.
 """
 from __future__ import annotations
 
@@ -136,6 +145,9 @@ def main():
                          "1.9%% of a whole frame's render (profiles/r01_shard_probe_c2_root.log)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-baseline budget (rank 0, N=1); 0 disables")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (default 0: every core this process may use -- nproc, bounded by a "
+                         "cgroup CPU quota)")
     ap.add_argument("--dump", default="", help="write the rank-0 frame as PNG here")
     ap.add_argument("--path", default="fused", choices=["fused", "wavefront"],
                     help="frame path: per-pixel megakernels (default) or wavefront stage kernels")
@@ -170,12 +182,32 @@ def main():
                          "two launches with the GI update on the side stream)")
     ap.add_argument("--flags", type=int, default=None,
                     help="experiments only: override the config's RV_F_* flags")
+    ap.add_argument("--alt-mode", type=int, default=1,
+                    help="reference frames, native loop: after the timed region, time the other loop mode (per-frame "
+                         "pipelined launches vs grouped launches of --alt-group frames) and report both under "
+                         "\"modes\"; 0 = off")
+    ap.add_argument("--alt-group", type=int, default=16,
+                    help="frames per launch of the grouped mode the alternate leg times (default 16)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="no GPU: only the rank plumbing (spawn or launcher, gloo process group, barrier, max-over-"
+                         "ranks timing) and one JSON line -- the CPU test of --gpus N")
     ap.add_argument("--dropin-leg", type=int, default=1,
                     help="one GPU, native loop, reference frames (C3-C5): after the timed region, time the same "
                          "number of frames through renderLoop's own calls (rv_update_gi_data, then rv_draw_cuda, "
                          "one frame per call, no knowledge of the next camera: src/main.cpp:119-132) and report "
                          "them as \"dropin\" (ms/frame, cold latency, that loop's roofline); 0 = off")
     args = ap.parse_args()
+
+    # --gpus N: under a launcher WORLD_SIZE must agree; without one, start the N ranks here, before any
+    # GPU call (this process never initialises the GPU: it only waits for its children)
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is None and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    if env_ws is not None and int(env_ws) != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_ws} ranks")
+        return 2
+    if args.rehearse:
+        return rehearse(args)
 
     import torch
     import rvgrt_amd as rv
@@ -211,12 +243,12 @@ def main():
     atlas = load_atlas()
 
     # ---------------------------------------------------------------- world
+    r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=flags, atlas=atlas, device=local_rank)
     if world_size > 1:
         # N > 1: the native loop's groups alternate over two streams, so one group's tail overlaps the
         # next (one rank's C2 share at 8 ranks 19.6 -> 19.1 us/frame, profiles/r01_shard_probe_c2_streams.log);
         # one GPU keeps one stream so each launch runs alone and its event time is the kernel's own
-        os.environ.setdefault("RV_BATCH_STREAMS", "2")
-    r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=flags, atlas=atlas, device=local_rank)
+        r.set_option(rv.RV_OPT_BATCH_STREAMS, 2)
     # the frame stream runs at the highest priority: the library's GI side
     # stream is created at the lowest, so the GI kernel fills the frame's gaps
     stream = torch.cuda.Stream(device=dev, priority=args.stream_priority) if args.stream_priority else \
@@ -247,10 +279,12 @@ def main():
     # at 8 / 16, C5 198.1 -> 122.0 -> 114.1, at 4 ranks C4 182.4 -> 162.0 at 16.  Throughput-bound launches
     # keep the per-frame pipeline: C4 one GPU 0.491 -> 0.553 ms at 16, a 2-rank C4 share 278.9 -> 307.5 us.
     # The library caps the group by the GI grid (two groups' updates never overlap).
-    rank_waves = (W * H // 64) // max(world_size, 1)
-    group = args.group if args.group is not None else \
-        ((8 if world_size == 1 else 16) if gi_per_frame and prepass and args.pipe and args.path == "fused"
-         and rank_waves <= 49152 else 0)
+    # The mode is the one N = 1 runs for this config at every N (like-for-like scaling): C3's 1080p frame
+    # (32 K waves) groups 8 frames, C4/C5 (130 K waves) run one pipelined launch per frame.  The other mode
+    # is timed after the main region (--alt-mode).
+    ref_frames = gi_per_frame and prepass and args.pipe and args.path == "fused"
+    one_gpu_waves = W * H // 64
+    group = args.group if args.group is not None else (8 if ref_frames and one_gpu_waves <= 49152 else 0)
     r.set_frame_group(group)
     t0 = time.perf_counter()
     r.world_build()
@@ -273,7 +307,9 @@ def main():
     # starts again -- the warm-up and timed frames are the same frames (the same views) with or without it
     settle = max(0, args.settle - args.warmup)
     w0 = args.warmup                              # the first timed frame of the path
-    n_path = max(w0 + args.steps + n_stage_frames + 9 + 2 + 5 * max(group, 0), settle + 1)   # + the group-latency calls
+    alt_group = 0 if group >= 2 else max(2, args.alt_group)   # the alternate leg's frames per launch
+    n_alt = (args.warmup + args.steps + 2 * max(alt_group, 1) + 5 * alt_group) if args.alt_mode else 0
+    n_path = max(w0 + args.steps + n_stage_frames + 9 + 2 + 5 * max(group, 0) + n_alt, settle + 1)   # + the group-latency calls
     pan = args.pan if args.camera == "path" else 0.0
     path = camera_path((pos, yaw, pitch), W, H, n_path, pan=pan, ref_compat=args.camera == "path")
     if args.camera == "static":   # the round-1 bench: one camera, time 0, no jitter
@@ -345,15 +381,15 @@ def main():
     serial = [False]        # timing pass: every frame on streams[0]
     native = args.loop == "native" and (world_size == 1 or args.dist_backend == "nccl")
     comm = None
+    root_weight = None
     if native and world_size > 1:
         # RCCL communicator of the library (joins torch's librccl); id from rank 0.
         # Any rank that cannot load RCCL or create its side makes every rank
         # fall back to the Python loop's torch.distributed gather.
-        w0 = args.root_weight if args.root_weight is not None else 1.0 - 0.019 * (world_size - 1)
-        os.environ["RV_SHARD_ROOT_WEIGHT"] = repr(w0)   # read by rv_set_tile_shard; identical on every rank
-        r.set_tile_shard(T, rank, world_size)
+        root_weight = args.root_weight if args.root_weight is not None else 1.0 - 0.019 * (world_size - 1)
+        r.set_tile_shard(T, rank, world_size, root_weight=root_weight)   # identical on every rank
         from rvgrt_amd.tiles import shard_owners
-        my_tiles = np.flatnonzero(shard_owners(W, H, T, world_size, w0) == rank).astype(np.int32)
+        my_tiles = np.flatnonzero(shard_owners(W, H, T, world_size, root_weight) == rank).astype(np.int32)
         uid = torch.zeros(rv.Comm.ID_BYTES + 1, dtype=torch.uint8, device=dev)
         if rank == 0:
             try:
@@ -551,6 +587,52 @@ def main():
             gl.append((time.perf_counter() - t1) * 1000.0)
         group_latency_ms = round(float(np.median(gl)), 4)
 
+    # ---------------------------------------------------------------- the other loop mode
+    # Reference frames in the native loop: the same context, world and camera path (continued), timed in the
+    # mode the main region did not run -- per-frame pipelined launches vs grouped launches -- so both modes'
+    # 1 -> N curves exist, each like with like.
+    modes = None
+    if args.alt_mode and native and ref_frames and bool(flags & rv.RV_F_PREPASS):
+        def max_over_ranks(v):
+            if dist is None:
+                return v
+            t = torch.tensor([v], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+        main_ms = elapsed * 1000.0 / args.steps
+        main_name = "grouped" if ref_group >= 2 else "per_frame"
+        modes = {main_name: {"frames_per_launch": ref_group if ref_group >= 2 else 1, "ms_per_step": round(main_ms, 4),
+                             "value": round(rays_per_frame / main_ms / 1e3, 2), "latency_ms": group_latency_ms
+                             if ref_group >= 2 else latency_ms, "steps": args.steps, "is_value": True}}
+        r.set_frame_group(alt_group)
+        eff = r.frame_group_effective()
+        per = eff if eff >= 2 else 1
+        n_alt_steps = ((args.steps + per - 1) // per) * per
+        run_native(((max(args.warmup, per) + per - 1) // per) * per)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        run_native(n_alt_steps)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        alt_el = max_over_ranks(time.perf_counter() - t1)
+        al = []
+        for _ in range(3):
+            barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            run_native(per)
+            torch.cuda.synchronize(dev)
+            al.append((time.perf_counter() - t1) * 1000.0)
+        alt_ms = alt_el * 1000.0 / n_alt_steps
+        modes["grouped" if eff >= 2 else "per_frame"] = {
+            "frames_per_launch": per, "ms_per_step": round(alt_ms, 4),
+            "value": round(rays_per_frame / alt_ms / 1e3, 2), "latency_ms": round(float(np.median(al)), 4),
+            "steps": n_alt_steps, "is_value": False}
+        r.set_frame_group(group)
+
     gather_check = None
     if world_size > 1 and rank == 0:   # the gathered frame must equal a one-GPU frame
         tiled = r.readback(rv.RV_IMAGE_COLOR).copy()
@@ -642,7 +724,7 @@ def main():
     # ---------------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and world_size == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(r, cfg, path[w0], flags, atlas, args.cpu_seconds)
+        cpu = cpu_baseline(r, cfg, path[w0], flags, atlas, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         line = {
@@ -686,9 +768,11 @@ def main():
             # their half-res window themselves (rv_flow_info; 0 = every tile arrived through the hand-off)
             "flow_fallbacks": r.flow_info()[2] if flowed else None,
             "frame_group": ref_group,
+            # both loop modes of the reference frame (value = the "is_value" one, the mode N = 1 runs)
+            "modes": modes,
             "loop": "native" if native else "python",
             "gather": ("rccl" if native else args.dist_backend) if world_size > 1 else None,
-            "root_weight": float(os.environ.get("RV_SHARD_ROOT_WEIGHT", "1")) if world_size > 1 and native else None,
+            "root_weight": root_weight if world_size > 1 and native else None,
             "gather_check": gather_check,
             "roofline": roofline,
             "dropin": dropin,
@@ -703,6 +787,69 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher: N child processes of this script, one per GPU, with the
+    environment torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR /
+    MASTER_PORT on 127.0.0.1).  This parent never touches the GPU; it relays rank 0's stdout (the JSON
+    line) and returns the first non-zero exit status (a failed rank ends the others)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for rk in range(n):
+        env = dict(os.environ, RANK=str(rk), LOCAL_RANK=str(rk), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if rk == 0 else sys.stderr, start_new_session=True))
+    out = procs[0].communicate()[0]
+    rcs = [procs[0].returncode]
+    for p in procs[1:]:
+        try:
+            rcs.append(p.wait(timeout=60 if rcs[0] == 0 else 10))
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            rcs.append(p.wait())
+    for ln in out.decode(errors="replace").splitlines(keepends=True):   # the JSON line(s) to stdout, noise to stderr
+        (sys.stdout if ln.startswith("{") else sys.stderr).write(ln)
+    sys.stdout.flush()
+    bad = [c for c in rcs if c != 0]
+    if bad:
+        log(f"bench.py: rank exit codes {rcs}")
+    return bad[0] if bad else 0
+
+
+def rehearse(args) -> int:
+    """--rehearse: the multi-rank plumbing without a GPU -- a gloo process group over the ranks, the
+    barrier-bracketed timed region (a host-side stand-in for the frames) and the max over ranks -- and
+    rank 0's JSON line.  tests/test_bench_cli.py runs it on the CPU."""
+    import torch
+    import torch.distributed as dist
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if ws > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.001 * (1 + rank))
+    if ws > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "rehearsal (no GPU)", "value": None, "n_gpus": ws, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(el * 1000.0 / max(args.steps, 1), 4),
+                          "rehearsal": True, "ranks_timed": ws}), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def dropin_leg(r, stream, cfg, flags, pos, yaw, pitch, pan, args, gi_stats, traffic_dir):
@@ -797,7 +944,21 @@ def dropin_leg(r, stream, cfg, flags, pos, yaw, pitch, pan, args, gi_stats, traf
                                           if traffic and launch_ms > 0 else None)}}
 
 
-def cpu_baseline(r, cfg, d, flags, atlas, budget_s):
+def host_cores():
+    """(nproc, cgroup CPU quota in whole cores or None): nproc is what `nproc` prints (the affinity mask)."""
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return nproc, quota
+
+
+def cpu_baseline(r, cfg, d, flags, atlas, budget_s, args_cpu_threads=0):
     """The CPU oracle (scalar DDA restatement, oracle/rv_oracle.c) on the host
     cores: same world (exported from the GPU; bit-identical to the oracle's
     own build, tests/test_gpu_parity.py), same camera and features, the frame
@@ -809,7 +970,10 @@ def cpu_baseline(r, cfg, d, flags, atlas, budget_s):
     import rvgrt_amd as rv
     from oracle import oracle as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    nproc, quota = host_cores()
+    # all the host cores this process may use: nproc (its CPU affinity), bounded by a cgroup CPU quota when
+    # one is set (a GPU box's share of a larger machine); --cpu-threads overrides
+    threads = args_cpu_threads or (min(nproc, quota) if quota else nproc)
     O.set_threads(threads)
     w = O.OracleWorld(cfg.log2_n, cfg.log2_n, cfg.log2_n, atlas=atlas)
     w.bits[:] = r.world_export(rv.RV_WORLD_BITS)
@@ -843,6 +1007,7 @@ def cpu_baseline(r, cfg, d, flags, atlas, budget_s):
     O.set_threads(threads)
     what = (f"stride-{stride} row subset ({len(rows_all)} of {H} rows)" if stride > 1 else "whole frames")
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cgroup_cpu_quota": quota,
             "value_1core": round(rays1 / dt1 / 1e6, 3),
             "sample": f"oracle/rv_oracle.c render of {what} of {cfg.name}: {rows} rows ({rows / H:.2f} frame "
                       f"heights) in {chunk}-row chunks on {threads} threads, {dt:.1f} s wall, {rays} traces, "
@@ -850,4 +1015,4 @@ def cpu_baseline(r, cfg, d, flags, atlas, budget_s):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -22,17 +22,11 @@
 #ifndef RV_G_PREPASS      // distApproximationKernel: the longest chains (camera ray + shadow ray)
 #define RV_G_PREPASS 8    // 8 (68 VGPRs: the pipelined launch at 7 waves/SIMD) beats 4 at 8 waves:
 #endif                    // C4 0.535 -> 0.512 ms, C5 0.782 -> 0.731, C3 -1.5 % (profiles/r02/lookahead_ab.txt)
-#ifndef RV_PRIMARY_TILE   // render primary rays: a 2x2x2-brick LDS tile around the wave's ray starts
-#define RV_PRIMARY_TILE 0
-#endif
 #ifndef RV_LATE_MATRICES  // pipelined launch: load the MV/depth matrices where they are used (SGPR pressure)
 #define RV_LATE_MATRICES 1   // 106 -> 97 SGPRs, 7 -> 8 waves/SIMD: C4 0.631 -> 0.603 ms (profiles/r02/rewalk_ab.txt)
 #endif
 #ifndef RV_HALF_WINDOW    // minDist / bilinear taps from an LDS window of the wave's half-res texels
 #define RV_HALF_WINDOW 0   // measured C4 0.678 (off) vs 0.688 ms (on), C3 equal: the taps are not the limit
-#endif
-#ifndef RV_CONES_BATCHED  // the six cones' first-step gathers issued together (trace_cones6)
-#define RV_CONES_BATCHED 1
 #endif
 #ifndef RV_G_REFL         // the water reflection ray's look-ahead (0: the frame's G); A/B builds
 #define RV_G_REFL 0
@@ -83,10 +77,7 @@ __device__ inline void refl_diag_add(uint32_t n) {
 struct NoPublish { __device__ void operator()(float) const {} };
 // on_dist(d - 8): called once the camera ray is done, before the shadow ray (the flow launch publishes the
 // distance there: the two-phase hand-off, rv_kernels.hip flow_pre_part)
-#ifndef RV_SPEC_PP   // the pre-pass rays' speculative sphere steps (rv_device.h trace SPEC: 0, 1 or 3)
-#define RV_SPEC_PP 0
-#endif
-template <bool STATS, class WV = World, int G = RV_G_PREPASS, class PUB = NoPublish, int SPEC = RV_SPEC_PP>
+template <bool STATS, class WV = World, int G = RV_G_PREPASS, class PUB = NoPublish>
 __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, int ix, int iy,
                                              uint32_t (&c)[NCNT], float& dist_out, float& shadow_out,
                                              const PUB& on_dist = PUB()) {
@@ -95,15 +86,15 @@ __device__ __forceinline__ void prepass_eval(const WV& w, const FrameParams& f, 
     f3 dir = ray_dir(f, x, y);
     StepCount sc{};
     RV_GD_KIND(gd::PP_PRIMARY);
-    Hit h = trace<STATS, G, false, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && (G > 1) && RV_DDA_REWALK, SPEC>(
+    Hit h = trace<STATS, G, false, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && (G > 1) && RV_DDA_REWALK>(
         w, f.pos, dir, 0.0f, sc);
     float d = h.hit ? length(sub(h.pos, f.pos)) : 300.0f;
     float s = 1.0f;
     on_dist(d - 8.0f);
     if (STATS) { c[CNT_TRACES]++; c[CNT_PP_PRIMARY]++; c[CNT_UNDEF] += h.undef; }
-    if (h.hit && !(RV_ABLATE & 1024)) {
+    if (h.hit) {
         RV_GD_KIND(gd::PP_SHADOW);
-        Hit sh = trace_sun<STATS, G, false, WV, (RV_COL_SUN != 0) && (G > 1) && (RV_DDA_REWALK != 0), SPEC>(
+        Hit sh = trace_sun<STATS, G, false, WV, (RV_COL_SUN != 0) && (G > 1) && (RV_DDA_REWALK != 0)>(
             w, add(h.pos, scale(h.normal, 1e-1f)), f.sun, 0.0f, sc);
         s = sh.hit ? SHADOW_HIT : 1.0f;
         if (STATS) { c[CNT_TRACES]++; c[CNT_PP_SHADOW]++; }
@@ -157,6 +148,28 @@ template <uint32_t FEAT> struct TraceCfg {
     static constexpr bool REUSE = !REF && RV_REUSE_FRAME;
 };
 
+// The land branch's indirect light (StateRender.cu:100-127): the 6 cones of a hit (up, lerp(up, +-right,
+// .5), lerp(up, +-fwd, .5), lerp(up, lerp(right, fwd, .5), .5) -- not normalised, R12) from the GI grid,
+// their first-step gathers issued together (trace_cones6), and the sky ambient.
+template <bool STATS, int CB, class WV>
+__device__ __forceinline__ void cone_lighting(const WV& w, const FrameParams& f, const Hit& hit, f3 base,
+                                              uint32_t (&c)[NCNT], f3& ind, f3& amb) {
+    f3 up = hit.normal;
+    f3 right, fwd;
+    if ((up.x != 0.0f) | (up.y != 0.0f) | (up.z != 0.0f)) {   // axis normal: constant scales
+        right = scale(cross(up, V(0.577f, 0.577f, 0.577f)), f.cone_k1);
+        fwd = scale(cross(up, right), f.cone_k2);
+    } else {
+        right = normalize(cross(up, V(0.577f, 0.577f, 0.577f)));
+        fwd = normalize(cross(up, right));
+    }
+    uint32_t steps = 0;
+    ind = trace_cones6<STATS, CB>(w, hit.pos, up, right, fwd, steps);
+    if (STATS) { c[CNT_CONES] += 6; c[CNT_CONE_STEPS] += steps; }
+    ind = scale(mul(divs(ind, 6.0f), base), 0.6f);
+    amb = mul(scale(sample_sky(hit.normal, f.sun), 0.05f), base);
+}
+
 // computeColor (StateRender.cu:33-146)
 // COLOK: the launch may take the water reflection's column skip (k_ref_flow: no -- its render waits inside
 // the launch and the skip's registers cost it 3.5 %, profiles/r04/col_skip_atlas_ab.txt)
@@ -174,69 +187,31 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
     constexpr int G = GR ? GR : TraceCfg<FEAT>::G;
     constexpr bool RE = TraceCfg<FEAT>::REUSE;
     RV_GD_KIND(gd::PRIMARY);
-#if RV_PRIMARY_TILE
-    // the wave's primary rays start within a few voxels of each other, just before their surface
-    // (minDist - 8): the 2x2x2 bricks around the first lane's start, extended along its direction,
-    // go to LDS with one 16-B load per lane and serve the in-tile sphere / DDA gathers
-    if (prepass && __ballot(1) == ~0ull) {
-        __shared__ uint32_t s_tile[256];
-        const f3 st = add(f.pos, scale(dir, hround(dist)));
-        const int fx = __builtin_amdgcn_readfirstlane((int)floorf(st.x));
-        const int fy = __builtin_amdgcn_readfirstlane((int)floorf(st.y));
-        const int fz = __builtin_amdgcn_readfirstlane((int)floorf(st.z));
-        const int nx = __builtin_amdgcn_readfirstlane(dir.x < 0.0f), ny = __builtin_amdgcn_readfirstlane(dir.y < 0.0f),
-                  nz = __builtin_amdgcn_readfirstlane(dir.z < 0.0f);
-        WorldTile wt;
-        static_cast<World&>(wt) = w;
-        wt.tile = s_tile;
-        wt.tbx = (uint32_t)imin(imax((fx >> 3) - nx, 0), (w.X >> 3) - 2);
-        wt.tby = (uint32_t)imin(imax((fy >> 3) - ny, 0), (w.Y >> 3) - 2);
-        wt.tbz = (uint32_t)imin(imax((fz >> 3) - nz, 0), (w.Z >> 3) - 2);
-        const uint32_t l = threadIdx.x & 63u, r = l >> 5, q = (l >> 2) & 7u, piece = l & 3u;
-        const uint32_t off = brick_byte(w, wt.tbx + (q & 1u), wt.tby + ((q >> 1) & 1u), wt.tbz + (q >> 2)) +
-                             (r ? w.coff : 0u) + piece * 16u;
-        const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(w.brick) + off);
-        *reinterpret_cast<uint4*>(&s_tile[r * 128u + q * 16u + piece * 4u]) = v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        hit = trace<STATS, G, RE>(wt, f.pos, dir, hround(dist), sc);
-    } else
-#endif
     hit = trace<STATS, G, RE, (RV_DDA_REWALK != 0), false, WV, RV_COL_PRIMARY && GR == 0 && (G > 1) && RV_DDA_REWALK>(
         w, f.pos, dir, hround(dist), sc);
     if (STATS) { c[CNT_TRACES]++; c[CNT_PRIMARY]++; c[CNT_UNDEF] += hit.undef; }
     f3 color;
-    if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER) && (RV_ABLATE & 4)) {
-        color = sample_sky(dir, f.sun);
-    } else if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER)) {
-        // timing ablations: 2048 the wave normal's two fbm3D, 8192 the reflection ray, 4096 its shadow ray
-        float nxw = (RV_ABLATE & 2048) ? 0.0f : fbm3D(hit.pos.x, hit.pos.z, f.time, 3, 0.06f, 2.0f, 0.6f);
-        float nyw = (RV_ABLATE & 2048) ? 0.0f : fbm3D(hit.pos.z, hit.pos.x, f.time + 112.0f, 3, 0.06f, 2.0f, 0.6f);
-        if (RV_ABLATE & 16384) { nxw = nxw * 0.0f; nyw = nyw * 0.0f; }   // timing: the noise computed, not used
+    if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER)) {
+        float nxw = fbm3D(hit.pos.x, hit.pos.z, f.time, 3, 0.06f, 2.0f, 0.6f);
+        float nyw = fbm3D(hit.pos.z, hit.pos.x, f.time + 112.0f, 3, 0.06f, 2.0f, 0.6f);
         f3 dn = normalize(add(hit.normal, V(nxw * 0.1f, nyw * 0.1f, 0.0f)));
         f3 rdir = reflect(dir, dn);
         RV_GD_KIND(gd::REFL);
-        Hit rh;
-        if (RV_ABLATE & 8192) rh.hit = false;
-        else {
-            constexpr int GG = RV_G_REFL ? RV_G_REFL : G;
-            constexpr bool COLR = RV_COL_REFL && (GG > 1) && RV_DDA_REWALK && GR == 0 && COLOK;   // throughput launches
+        constexpr int GG = RV_G_REFL ? RV_G_REFL : G;
+        constexpr bool COLR = RV_COL_REFL && (GG > 1) && RV_DDA_REWALK && GR == 0 && COLOK;   // throughput launches
 #if RV_REFL_DIAG
-            const uint32_t s0 = sc.sphere + sc.dda;
+        const uint32_t s0 = sc.sphere + sc.dda;
 #endif
-            rh = trace<STATS, GG, RE, (RV_DDA_REWALK != 0), false, WV, COLR>(w, hit.pos, rdir, hround(0.001f), sc);
+        Hit rh = trace<STATS, GG, RE, (RV_DDA_REWALK != 0), false, WV, COLR>(w, hit.pos, rdir, hround(0.001f), sc);
 #if RV_REFL_DIAG
-            if (STATS) refl_diag_add(sc.sphere + sc.dda - s0);
+        if (STATS) refl_diag_add(sc.sphere + sc.dda - s0);
 #endif
-        }
         if (STATS) { c[CNT_TRACES]++; c[CNT_REFL]++; }
         f3 rc;
         if (rh.hit) {
             rc = sample_texture(w, rh.u, rh.v, rh.pos);
             RV_GD_KIND(gd::REFL_SHADOW);
-            Hit rs;
-            if (RV_ABLATE & 4096) rs.hit = false;
-            else rs = trace_sun<STATS, G, RE>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
+            Hit rs = trace_sun<STATS, G, RE>(w, add(rh.pos, scale(rh.normal, 1e-3f)), f.sun, hround(0.001f), sc);
             if (STATS) { c[CNT_TRACES]++; c[CNT_REFL_SHADOW]++; c[CNT_TEX]++; }
             if (rs.hit) rc = scale(rc, 0.1f);
         } else {
@@ -249,33 +224,6 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
         f3 base = sample_texture(w, hit.u, hit.v, hit.pos);
         if (STATS) c[CNT_TEX]++;
         float shadow = shadow_in;
-        if (DS && has<FEAT>(f, RV_F_GI) && !(RV_ABLATE & 2)) {   // the cones first, then the deferred shadow
-            float diffuse = fmaxf(dot(hit.normal, f.sun), 0.0f);
-            f3 up = hit.normal;
-            f3 right, fwd;
-            if ((up.x != 0.0f) | (up.y != 0.0f) | (up.z != 0.0f)) {
-                right = scale(cross(up, V(0.577f, 0.577f, 0.577f)), f.cone_k1);
-                fwd = scale(cross(up, right), f.cone_k2);
-            } else {
-                right = normalize(cross(up, V(0.577f, 0.577f, 0.577f)));
-                fwd = normalize(cross(up, right));
-            }
-            uint32_t steps = 0;
-            f3 ind = trace_cones6<STATS, CB>(w, hit.pos, up, right, fwd, steps);
-            if (STATS) { c[CNT_CONES] += 6; c[CNT_CONE_STEPS] += steps; }
-            ind = scale(mul(divs(ind, 6.0f), base), 0.6f);
-            f3 amb = mul(scale(sample_sky(hit.normal, f.sun), 0.05f), base);
-            if (prepass) {
-                resolve_shadow_taps(f, x, y, hwin);
-                shadow = bilinear_tex(f, x, y, hwin);
-            }
-            f3 direct = scale(scale(base, diffuse), shadow);
-            color = add(add(direct, ind), amb);
-        } else {
-        if (DS && prepass) {
-            resolve_shadow_taps(f, x, y, hwin);
-            shadow = bilinear_tex(f, x, y, hwin);
-        }
         if (!prepass) {
             shadow = 1.0f;
             if (has<FEAT>(f, RV_F_SHADOW)) {
@@ -286,43 +234,19 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
             }
         }
         float diffuse = fmaxf(dot(hit.normal, f.sun), 0.0f);
+        f3 ind, amb;
+        const bool gi = has<FEAT>(f, RV_F_GI);
+        if (gi) cone_lighting<STATS, CB>(w, f, hit, base, c, ind, amb);   // DS: the cones before the shadow taps
+        if (DS && prepass) {
+            resolve_shadow_taps(f, x, y, hwin);
+            shadow = bilinear_tex(f, x, y, hwin);
+        }
         f3 direct = scale(scale(base, diffuse), shadow);
-        if (has<FEAT>(f, RV_F_GI) && (RV_ABLATE & 2)) {
-            color = direct;
-        } else if (has<FEAT>(f, RV_F_GI)) {
-            f3 up = hit.normal;
-            f3 right, fwd;
-            if ((up.x != 0.0f) | (up.y != 0.0f) | (up.z != 0.0f)) {   // axis normal: constant scales
-                right = scale(cross(up, V(0.577f, 0.577f, 0.577f)), f.cone_k1);
-                fwd = scale(cross(up, right), f.cone_k2);
-            } else {
-                right = normalize(cross(up, V(0.577f, 0.577f, 0.577f)));
-                fwd = normalize(cross(up, right));
-            }
-            uint32_t steps = 0;
-#if RV_CONES_BATCHED
-            f3 ind = trace_cones6<STATS, CB>(w, hit.pos, up, right, fwd, steps);
-#else
-            f3 ind = trace_cone<STATS>(w, hit.pos, up, steps);
-            ind = add(ind, trace_cone<STATS>(w, hit.pos, lerp(up, right, 0.5f), steps));
-            ind = add(ind, trace_cone<STATS>(w, hit.pos, lerp(up, neg(right), 0.5f), steps));
-            ind = add(ind, trace_cone<STATS>(w, hit.pos, lerp(up, fwd, 0.5f), steps));
-            ind = add(ind, trace_cone<STATS>(w, hit.pos, lerp(up, neg(fwd), 0.5f), steps));
-            ind = add(ind, trace_cone<STATS>(w, hit.pos, lerp(up, lerp(right, fwd, 0.5f), 0.5f), steps));
-#endif
-            if (STATS) { c[CNT_CONES] += 6; c[CNT_CONE_STEPS] += steps; }
-            ind = scale(mul(divs(ind, 6.0f), base), 0.6f);
-            f3 amb = mul(scale(sample_sky(hit.normal, f.sun), 0.05f), base);
-            color = add(add(direct, ind), amb);
-        } else {
-            color = direct;
-        }
-        }
+        color = gi ? add(add(direct, ind), amb) : direct;
     } else {
         color = sample_sky(dir, f.sun);
     }
     if (STATS) { c[CNT_SPHERE] += sc.sphere; c[CNT_DDA] += sc.dda; c[CNT_CHECK] += sc.check; }
-    if (RV_ABLATE & 8) return color;
     float fog = hit.hit ? fog_pow(length(sub(hit.pos, f.pos)) * 0.0004f) : 1.0f;
     return add(scale(color, fog), scale(V(0.95f, 0.95f, 1.0f), 1.0f - fog));
 }
@@ -382,11 +306,11 @@ __device__ __forceinline__ uint32_t render_pixel(const WV& w, const FrameParams&
     RV_GD(1, reinterpret_cast<char*>(f.depth) + (size_t)iy * f.depth_pitch + 2 * (size_t)ix);
     RV_GD(2, reinterpret_cast<char*>(f.color) + (size_t)iy * f.color_pitch + 4 * (size_t)ix);
     // images are < 4 GiB: 32-bit byte offsets on the SGPR base
-    if (f.mv && !(RV_ABLATE & 16)) {
+    if (f.mv) {
         uint32_t m = (uint32_t)hbits(mvx) | ((uint32_t)hbits(-mvy) << 16);
         out_store(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(f.mv) + ((uint32_t)iy * (uint32_t)f.mv_pitch + 4u * (uint32_t)ix)), m);
     }
-    if (f.depth && !(RV_ABLATE & 16)) {
+    if (f.depth) {
         out_store(reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(f.depth) + ((uint32_t)iy * (uint32_t)f.depth_pitch + 2u * (uint32_t)ix)),
                   hbits(dep));
     }

@@ -19,6 +19,11 @@ RV_FLAGS_REFERENCE = RV_F_PREPASS | RV_F_WATER | RV_F_GI
 RV_IMAGE_COLOR, RV_IMAGE_MOTION, RV_IMAGE_DEPTH, RV_IMAGE_HALF_DIST, RV_IMAGE_HALF_SHADOW = range(5)
 RV_WORLD_BITS, RV_WORLD_CSDF, RV_WORLD_GI = range(3)
 RV_PATH_FUSED, RV_PATH_WAVEFRONT = 0, 1
+# rv_set_option (include/rvgrt.h rv_option)
+RV_OPT_PIPE_ORDER, RV_OPT_BATCH_STREAMS, RV_OPT_FLOW_SPIN, RV_OPT_FLOW_FORCE_FALLBACK, RV_OPT_GI_PAIRS, \
+    RV_OPT_GI_SHARD_PROBE = range(1, 7)
+# rv_config.exits_off bits
+RV_EXIT_SKY, RV_EXIT_COLUMN, RV_EXIT_SUN = 1, 2, 4
 
 STAGES = ["pp_primary", "pp_shadow", "primary", "shadow", "water", "cones", "shade", "gi"]
 STATUS_NAMES = {0: "RV_OK", 1: "RV_ERR_INVALID", 2: "RV_ERR_HIP", 3: "RV_ERR_OOM",
@@ -31,7 +36,8 @@ class rv_config(C.Structure):
                 ("seed_x", C.c_int32), ("seed_z", C.c_int32),
                 ("ref_compat", C.c_int32), ("ref_oob_jy", C.c_float),
                 ("atlas_rgba8", C.c_void_p), ("atlas_w", C.c_int32), ("atlas_h", C.c_int32),
-                ("gi_rays_per_frame", C.c_uint32), ("gi_init_saturate", C.c_int32)]
+                ("gi_rays_per_frame", C.c_uint32), ("gi_init_saturate", C.c_int32),
+                ("tex_table", C.c_int32), ("exits_off", C.c_int32)]
 
 
 class rv_camera(C.Structure):
@@ -73,6 +79,8 @@ SIGNATURES = [
     ("rv_destroy", None, [P]),
     ("rv_last_error", C.c_char_p, [P]),
     ("rv_set_stream", I32, [P, P]),
+    ("rv_set_option", I32, [P, I32, C.c_int64]),
+    ("rv_get_option", I32, [P, I32, C.POINTER(C.c_int64)]),
     ("rv_set_frame_path", I32, [P, I32]),
     ("rv_tile_shard_assign", I32, [I32, I32, I32, I32, C.c_float, P]),
     ("rv_set_gi_async", I32, [P, I32]),

@@ -80,34 +80,9 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
     c->slots.resize(1);
     if (!slot_alloc(c, c->slots[0])) return cleanup_fail(RV_ERR_OOM, "frame slot");
     slot_load(c, 0);
-    if (const char* e = getenv("RV_SCHED")) c->sched = atoi(e);
-    if (const char* e = getenv("RV_BATCH_STREAMS")) c->batch_streams = atoi(e);
-    if (const char* e = getenv("RV_GI_PRIO")) c->gi_low_prio = atoi(e);
-    if (const char* e = getenv("RV_ORDER_EVERY")) c->order_every = atoi(e) > 0 ? atoi(e) : 1;
-    if (const char* e = getenv("RV_PIPE")) c->pipe = atoi(e);
-    if (const char* e = getenv("RV_PIPE_CARRY")) c->pipe_carry = atoi(e);
-    if (const char* e = getenv("RV_FLOW")) c->flow = atoi(e);
-    if (const char* e = getenv("RV_GI_PAIRS")) c->gi_pairs = atoi(e);
-    if (const char* e = getenv("RV_PRIO_BLOCKS")) c->prio_blocks = (uint32_t)std::max(0, atoi(e));
-    if (const char* e = getenv("RV_FLOW_SPIN")) c->flow_spin = (uint32_t)std::max(0, atoi(e));
-    if (const char* e = getenv("RV_FLOW_FORCE_FALLBACK")) c->flow_force_fallback = atoi(e) != 0;
-    if (const char* e = getenv("RV_FLOW_PP_ORDER")) c->flow_pp_order = (uint32_t)(atoi(e) != 0);
-    if (const char* e = getenv("RV_FLOW_GI_SIDE")) c->flow_gi_side = atoi(e) != 0;
-    if (const char* e = getenv("RV_GROUP")) c->group = std::min(32, std::max(0, atoi(e)));
-    if (const char* e = getenv("RV_GATHER_BPP")) {   // 3 or 4; anything else is an error, not a silent default
-        if (strcmp(e, "3") != 0 && strcmp(e, "4") != 0) return cleanup_fail(RV_ERR_INVALID, "RV_GATHER_BPP");
-        c->gather_bpp = atoi(e);
-    }
-    if (const char* e = getenv("RV_PIPE_ORDER")) {   // a permutation of the parts, else the default
-        const uint32_t o = (uint32_t)strtoul(e, nullptr, 16);
-        const uint32_t a = o >> 8 & 0xF, b = o >> 4 & 0xF, d = o & 0xF;
-        if (o <= 0x210 && a < 3 && b < 3 && d < 3 && a != b && b != d && a != d) c->pipe_order = o;
-    }
     if (hipMalloc(&c->counters, NSTAGE * NCNT * sizeof(unsigned long long)) != hipSuccess)
         return cleanup_fail(RV_ERR_OOM, "counters");
     hipMemset(c->counters, 0, NSTAGE * NCNT * sizeof(unsigned long long));
-    if (const char* e = getenv("RV_MEGAKERNEL")) c->megakernel = atoi(e) != 0;
-    if (const char* e = getenv("RV_WF_ENQ")) c->enq = atoi(e);
     {   // wavefront stage buffers
         size_t npx = (size_t)W * H, nhalf = (size_t)(W / 2) * (H / 2);
         bool ok = hipMalloc(&c->hpos, npx * 16) == hipSuccess && hipMalloc(&c->hinfo, npx * 4) == hipSuccess &&
@@ -226,6 +201,53 @@ rv_status rv_set_stream(rv_ctx* c, void* s) {
     if (!c) return RV_ERR_INVALID;
     c->stream = (hipStream_t)s;
     return RV_OK;
+}
+
+rv_status rv_set_option(rv_ctx* c, int32_t opt, int64_t v) {
+    if (!c) return RV_ERR_INVALID;
+    switch (opt) {
+    case RV_OPT_PIPE_ORDER: {   // a permutation of the parts PIPE_GI / PIPE_PP / PIPE_RENDER
+        const uint32_t a = (uint32_t)(v >> 8 & 0xF), b = (uint32_t)(v >> 4 & 0xF), d = (uint32_t)(v & 0xF);
+        if (v < 0 || v > 0x210 || a > 2 || b > 2 || d > 2 || a == b || b == d || a == d)
+            return fail(c, RV_ERR_INVALID, "RV_OPT_PIPE_ORDER: not a permutation of 0, 1, 2");
+        c->pipe_order = (uint32_t)v;
+        c->carry_gi = c->carry_pp = false;
+        return RV_OK;
+    }
+    case RV_OPT_BATCH_STREAMS:
+        if (v != 1 && v != 2) return fail(c, RV_ERR_INVALID, "RV_OPT_BATCH_STREAMS: 1 or 2");
+        c->batch_streams = (int)v;
+        return RV_OK;
+    case RV_OPT_FLOW_SPIN:
+        if (v < 0 || v > (1 << 30)) return fail(c, RV_ERR_INVALID, "RV_OPT_FLOW_SPIN: 0 .. 2^30");
+        c->flow_spin = (uint32_t)v;
+        return RV_OK;
+    case RV_OPT_FLOW_FORCE_FALLBACK:
+        c->flow_force_fallback = v != 0;
+        return RV_OK;
+    case RV_OPT_GI_PAIRS:
+        if (v < -1 || v > 1) return fail(c, RV_ERR_INVALID, "RV_OPT_GI_PAIRS: -1, 0 or 1");
+        c->gi_pairs = (int)v;
+        return RV_OK;
+    case RV_OPT_GI_SHARD_PROBE:
+        c->gi_shard_probe = v != 0;
+        return RV_OK;
+    default:
+        return fail(c, RV_ERR_INVALID, "unknown option " + std::to_string(opt));
+    }
+}
+
+rv_status rv_get_option(rv_ctx* c, int32_t opt, int64_t* v) {
+    if (!c || !v) return RV_ERR_INVALID;
+    switch (opt) {
+    case RV_OPT_PIPE_ORDER: *v = c->pipe_order; return RV_OK;
+    case RV_OPT_BATCH_STREAMS: *v = c->batch_streams; return RV_OK;
+    case RV_OPT_FLOW_SPIN: *v = c->flow_spin; return RV_OK;
+    case RV_OPT_FLOW_FORCE_FALLBACK: *v = c->flow_force_fallback ? 1 : 0; return RV_OK;
+    case RV_OPT_GI_PAIRS: *v = c->gi_pairs; return RV_OK;
+    case RV_OPT_GI_SHARD_PROBE: *v = c->gi_shard_probe ? 1 : 0; return RV_OK;
+    default: return fail(c, RV_ERR_INVALID, "unknown option " + std::to_string(opt));
+    }
 }
 
 // Frames in flight: frame k takes slot k % n; its stream first waits for
@@ -404,13 +426,12 @@ rv_status rv_sync(rv_ctx* c) {
 // the kernels, with identical tiles -- so it is only allocated when it leaves room: the memory this
 // context may still allocate (CSDF build scratch, the GI scratch grid, two grouped-frame sets of 32
 // frames, the pipelined loop's buffers) plus 1 GiB, and at most half the device's free memory (other
-// contexts on the GPU).  Env RV_TEX_TABLE=0: never; =1: whenever the allocation succeeds.
+// contexts on the GPU).  rv_config.tex_table -1: never; 1: whenever the allocation succeeds.
 static rv_status tex_table(rv_ctx* c) {
     if (c->tex_tried) return RV_OK;
     c->tex_tried = true;
-    const char* te = getenv("RV_TEX_TABLE");
-    if (te && te[0] == '0') return RV_OK;
-    const bool force = te && te[0] == '1';
+    if (c->cfg.tex_table < 0) return RV_OK;
+    const bool force = c->cfg.tex_table > 0;
     const uint32_t ny = std::min((uint32_t)c->w.Y, (c->w.ytop + 7u) & ~7u);
     const size_t tb = (size_t)c->w.X * ny * c->w.Z * 4;
     if (!force) {
@@ -435,7 +456,7 @@ static rv_status tex_table(rv_ctx* c) {
 
 // The sky exit of the frame traversal (World::ytop, rv_device.h trace): the highest solid voxel
 // row + 2, and the sun exit of its shadow rays (World::horizon), recomputed after every write of the
-// bits.  Env RV_SKY_EXIT=0 turns both off (ytop = Y, no horizon).
+// bits.  rv_config.exits_off & RV_EXIT_SKY turns all three exits off (ytop = Y, no horizon, no skip).
 static rv_status world_top(rv_ctx* c) {
     c->w.ytop = (uint32_t)c->w.Y;
     uint32_t* hz = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->brick) + horizon_byte(c->w.coff));
@@ -443,8 +464,8 @@ static rv_status world_top(rv_ctx* c) {
     HIP_TRY(c, hipMemsetAsync(hz, 0xFF, hzb, c->stream));   // no sun exit unless built below
     int* dt = reinterpret_cast<int*>(reinterpret_cast<char*>(c->brick) + dtop_byte(c->w.coff, c->w.X, c->w.Z));
     HIP_TRY(c, hipMemsetAsync(dt, 0x7F, dtop_bytes(c->w.X, c->w.Z), c->stream));   // no column skip unless built below
-    const char* e = getenv("RV_SKY_EXIT");
-    if (e && e[0] == '0') return RV_OK;
+    const int off = c->cfg.exits_off;
+    if (off & RV_EXIT_SKY) return RV_OK;
     if (!c->d_top) HIP_TRY(c, hipMalloc(&c->d_top, 4));
     HIP_TRY(c, hipMemsetAsync(c->d_top, 0, 4, c->stream));
     launch_world_top(c->stream, c->brick, current_world(c), c->d_top);
@@ -453,19 +474,17 @@ static rv_status world_top(rv_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(&top, c->d_top, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->w.ytop = std::min((uint32_t)c->w.Y, top + 1u);   // top = max solid y + 1
-    // the column tops: the DDA's empty-column skip (dtop_at; env RV_COL_SKIP=0: off) and the sun horizon's input
+    // the column tops: the DDA's empty-column skip (dtop_at; RV_EXIT_COLUMN: off) and the sun horizon's input
     if (!c->coltop) HIP_TRY(c, hipMalloc(&c->coltop, hzb));
     HIP_TRY(c, hipMemsetAsync(c->coltop, 0, hzb, c->stream));
-    const char* cs = getenv("RV_COL_SKIP");
     launch_column_tops(c->stream, c->brick, current_world(c), c->coltop, dt);
     LAUNCH_CHECK(c);
-    if (cs && cs[0] == '0') HIP_TRY(c, hipMemsetAsync(dt, 0x7F, dtop_bytes(c->w.X, c->w.Z), c->stream));
+    if (off & RV_EXIT_COLUMN) HIP_TRY(c, hipMemsetAsync(dt, 0x7F, dtop_bytes(c->w.X, c->w.Z), c->stream));
     // the sun exit of shadow rays (trace_sun): the horizon per brick column for the library's sun
-    // (env RV_SUN_EXIT=0: off)
-    const char* se = getenv("RV_SUN_EXIT");
+    // (RV_EXIT_SUN: off)
     const f3 sun = sun_dir();
     const double hxz = std::sqrt((double)sun.x * sun.x + (double)sun.z * sun.z);
-    if ((se && se[0] == '0') || !(sun.y > 0.0f) || hxz == 0.0) return RV_OK;
+    if ((off & RV_EXIT_SUN) || !(sun.y > 0.0f) || hxz == 0.0) return RV_OK;
     // slope shaded 0.1 % low (a lower slope only raises the horizon: conservative)
     const float k = (float)((double)sun.y / hxz * (1.0 - 1e-3));
     launch_sun_horizon(c->stream, current_world(c), c->coltop, hz, (float)(sun.x / hxz), (float)(sun.z / hxz), k);
@@ -812,9 +831,9 @@ RV_HIDDEN rv_status run_stages(rv_ctx* c, FrameParams f, bool tiles, int which) 
                                    ((uint32_t)f.ntiles + 7u) & ~7u);
             } else {
                 launch_chunk_order(c->stream, pre ? c->chunk_cost[CG_PREPASS] : nullptr, c->chunk_order[CG_PREPASS],
-                                   n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh), chunks_x(f.hw),
+                                   n_chunks(f.hw, f.hh), n_chunks_pad(f.hw, f.hh),
                                    c->chunk_cost[CG_RENDER], c->chunk_order[CG_RENDER], n_chunks(f.W, f.H),
-                                   n_chunks_pad(f.W, f.H), chunks_x(f.W));
+                                   n_chunks_pad(f.W, f.H));
             }
             LAUNCH_CHECK(c);
         }
@@ -911,25 +930,13 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     p.gi_counters = c->counters + (size_t)ST_GI * NCNT;
     f.counters = c->counters + (size_t)ST_PRIMARY * NCNT;
     p.part[0] = PIPE_PP; p.part[1] = PIPE_GI; p.part[2] = PIPE_RENDER;
-    p.flow_pp_by_render = c->flow_pp_order;
-    if (const char* e = getenv("RV_FLOW_OPTS")) p.flow_opts = (uint32_t)atoi(e);   // A/B experiments
-    // pre-pass workgroups: 16 per render chunk slot in the render's order, or the pre-pass's own grid
-    p.len[0] = c->flow_pp_order ? n_chunks_pad(f.W, f.H) * 16u : pipe_len(f, PIPE_PP, 0);
+    if (RV_PIPE_DIAG)   // diagnostics builds only (tools/flow_waves.py): the pre-pass alone, one tile's waves
+        if (const char* e = getenv("RV_FLOW_OPTS")) p.flow_opts = (uint32_t)atoi(e);
+    // pre-pass workgroups: 16 per render chunk slot in the render's order
+    p.len[0] = n_chunks_pad(f.W, f.H) * 16u;
     p.len[2] = pipe_len(f, PIPE_RENDER, 0);
     p.gi_pairs = c->gi_pairs > 0 && pipe_latency_variant(f, p.len[2]) ? 1u : 0u;   // whole frames: off unless forced
-    const bool side = spec && c->flow_gi_side && c->gi_stream;
-    p.len[1] = spec && !side ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * count : count) : 0u;
-    if (side) {
-        // the GI stream starts once the grid this frame renders with is complete (every earlier write of
-        // `gi` and gi_tmp on the frame stream: the last copy-back included), then computes the window
-        // into gi_tmp beside the flow launch; the next rv_update_gi_data waits for ev_spec
-        if (!c->ev_spec) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
-        HIP_TRY(c, hipEventRecord(c->ev_spec, c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->gi_stream, c->ev_spec, 0));
-        launch_gi_update(c->gi_stream, c->gi, c->gi_tmp, current_world(c), sun_dir(), c->gi_frame, first, count,
-                         c->counters + ST_GI * NCNT, false);
-        LAUNCH_CHECK(c);
-    }
+    p.len[1] = spec ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * count : count) : 0u;
     p.flow_half = c->flow_half;
     p.flow_epoch = c->flow_epoch; p.flow_ntx = ntx;
     p.flow_expect = c->flow_force_fallback ? c->flow_epoch ^ 0x20000000u : c->flow_epoch;
@@ -964,21 +971,17 @@ static rv_status flow_frame(rv_ctx* c, FrameParams f) {
     }
     if (spec) {
         if (!c->ev_spec) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming));
-        HIP_TRY(c, hipEventRecord(c->ev_spec, side ? c->gi_stream : c->stream));
-        c->spec_stream = side ? c->gi_stream : c->stream;
+        HIP_TRY(c, hipEventRecord(c->ev_spec, c->stream));
+        c->spec_stream = c->stream;
         c->spec_rec = true;
         c->spec_gi = true;
         c->spec_fr = c->gi_frame; c->spec_first = first; c->spec_count = count; c->spec_world = c->world_ver;
     }
     if (f.sched == SCHED_COST && ++c->frames_since_order >= (uint32_t)c->order_every) {
         c->frames_since_order = 0;
-        // env RV_FLOW_REGIONS=1: a latency-variant flow frame (C3's 1080p) orders each XCD's chunks as one vertical
-        // strip of the image -- C3 P0 drop-in -1.1 %, P1 +5 % (profiles/r05/flow_regions_ab.txt): off by default
-        static const int flow_regions = [] { const char* e = getenv("RV_FLOW_REGIONS"); return e ? atoi(e) : 0; }();
-        const int regions = flow_regions && pipe_latency_variant(f, p.len[2]) ? 1 : -1;
         launch_chunk_order(c->stream, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                           n_chunks_pad(f.hw, f.hh), chunks_x(f.hw), c->chunk_cost[CG_RENDER],
-                           c->chunk_order[CG_RENDER], n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H), chunks_x(f.W), regions);
+                           n_chunks_pad(f.hw, f.hh), c->chunk_cost[CG_RENDER],
+                           c->chunk_order[CG_RENDER], n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H));
         LAUNCH_CHECK(c);
     }
     return RV_OK;

@@ -116,10 +116,10 @@ struct rv_ctx {
     bool gi_async = true;
     hipStream_t gi_stream = nullptr;
     int prio_lo = 0, prio_hi = 0;  // stream priority range (numerically: lo = least urgent)
-    int gi_low_prio = 1;           // RV_GI_PRIO: 1 = GI stream at the lowest priority (fills the frame's gaps)
+    int gi_low_prio = 1;           // 1 = GI stream at the lowest priority (fills the frame's gaps)
     hipEvent_t ev_world = nullptr;    // recorded on `stream` after the last world/GI write
     hipEvent_t ev_gi_done = nullptr;  // recorded on gi_stream after a GI kernel
-    int enq = 1;                  // RV_WF_ENQ: queue append granularity (FrameParams::enq)
+    int enq = 1;                  // wavefront path: queue append granularity (FrameParams::enq)
     // wavefront buffers
     float4* hpos = nullptr; uint32_t* hinfo = nullptr; float4* hsec = nullptr; float4* pphit = nullptr;
     int* wq[NQUEUE] = {nullptr, nullptr, nullptr, nullptr};
@@ -131,9 +131,9 @@ struct rv_ctx {
     uint64_t gi_offset = 0;
     bool world_ready = false;
     int sched = SCHED_COST;
-    int order_every = 4;          // RV_ORDER_EVERY: frames between chunk re-orderings
-    int pipe = 1;                 // rv_set_pipeline / RV_PIPE: pipelined reference frames
-    uint32_t pipe_order = 0x102;  // RV_PIPE_ORDER: dispatch order, hex digits PIPE_* (first = high): pre-pass, GI, render
+    int order_every = 4;          // frames between chunk re-orderings
+    int pipe = 1;                 // rv_set_pipeline: pipelined reference frames
+    uint32_t pipe_order = 0x102;  // RV_OPT_PIPE_ORDER: dispatch order, hex digits PIPE_* (first = high): pre-pass, GI, render
     float* pipe_half[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [k & 1] {dist, shadow}
     bool gi_stats = false;        // rv_set_gi_stats
     // pipelined tile loop: packed tiles / rank-0 gather buffers per frame parity, GI shard staging
@@ -148,7 +148,7 @@ struct rv_ctx {
     uint32_t* flow_wtrace = nullptr; uint32_t flow_wtrace_n = 0, flow_wlen[3] = {0, 0, 0};
     uint32_t pipe_launches = 0;
     uint32_t pipe_wnb[64] = {};       // workgroups of each recorded launch
-    int gather_bpp = 3;           // RV_GATHER_BPP: packed pixel bytes of rv_render_frames' tile gather (3 or 4)
+    int gather_bpp = 3;           // rv_set_gather_bpp: packed pixel bytes of rv_render_frames' tile gather (3 or 4)
     uint32_t frames_since_order = 0;
     int* chunk_order[2] = {nullptr, nullptr};      // SCHED_COST feedback per grid (CG_*)
     uint32_t* chunk_cost[2] = {nullptr, nullptr};
@@ -158,7 +158,7 @@ struct rv_ctx {
     hipStream_t comm_stream = nullptr;   // rv_render_frames: RCCL gathers, in frame order
     hipEvent_t ev_loop = nullptr;        // scratch event of rv_render_frames
     BatchSet bsets[2];
-    int batch_streams = 1;               // RV_BATCH_STREAMS: streams rv_render_frames' groups alternate over
+    int batch_streams = 1;               // RV_OPT_BATCH_STREAMS: streams rv_render_frames' groups alternate over
     // rv_set_tile_shard: this rank's tiles and the gathered layout (rank 0)
     int shard_px = 0, shard_rank = 0, shard_n = 0, shard_max = 0;
     std::vector<int32_t> shard_ids, shard_all;
@@ -172,7 +172,7 @@ struct rv_ctx {
     uint32_t carry_fr = 0; uint64_t carry_first = 0, carry_count = 0, carry_world = 0, carry_geom = 0;
     uint64_t carry_chunk = 0; int carry_n = 0, carry_r = 0, carry_half = 0;
     float carry_key[24] = {};
-    int pipe_carry = 1;            // RV_PIPE_CARRY
+    int pipe_carry = 1;            // the next frame's GI update and pre-pass are kept between calls
     // Flow frames (rv_set_flow; rv_frame / rv_draw_cuda of a frame with the pre-pass): one k_ref_flow
     // launch per frame.  Tile-major half-res hand-off buffer, per-tile flags, the launch epoch and the
     // count of render waves that fell back to evaluating their window.
@@ -182,22 +182,14 @@ struct rv_ctx {
     unsigned long long* flow_fb = nullptr;
     hipEvent_t ev_flow = nullptr;   // recorded after every flow launch, on the stream it ran on
     uint64_t flow_launches = 0;
-    // env RV_GI_PAIRS: latency-variant launches trace a GI cell's two rays on a lane pair (1 all, 0 none);
+    // RV_OPT_GI_PAIRS: latency-variant launches trace a GI cell's two rays on a lane pair (1 all, 0 none);
     // default -1: a rank's tile share only -- its GI part is 1/N of the cells and its longest GI waves
     // were the launch's floor (8-rank C4 share 137.4 -> 132.8 us/frame, GI longest wave 127.5 -> 98.9 us),
     // while a whole C3 frame's GI waves double for no gain (0.204 -> 0.240 ms; profiles/r04/gi_pairs_ab.txt)
     int gi_pairs = -1;
-    uint32_t prio_blocks = 0;        // env RV_PRIO_BLOCKS: leading pipelined-launch workgroups per part at high issue priority
-    uint32_t flow_spin = 16384;      // env RV_FLOW_SPIN: polls before a render wave evaluates its window
-    bool flow_force_fallback = false;   // env RV_FLOW_FORCE_FALLBACK=1 (tests): no wave waits, all evaluate
-    // env RV_FLOW_PP_ORDER: 1 (default) pre-pass tiles in the render's chunk order, so the tiles the first
-    // render waves read are published first (C3 -2 %, C4 -0.2 %, render waves finding a tile unpublished
-    // on arrival 330 -> 130 per C4 frame: profiles/r04/flow_ab.txt); 0 the pre-pass's own cost order
-    uint32_t flow_pp_order = 1;
-    // env RV_FLOW_GI_SIDE=1: the next UpdateGIData's cells of a flow frame run as their own GI kernel on the
-    // low-priority GI stream beside the flow launch (which then holds pre-pass + render only) instead of as
-    // the flow launch's GI part; same cells, same kernel body, consumed the same way (ev_spec)
-    bool flow_gi_side = false;
+    uint32_t flow_spin = 16384;      // RV_OPT_FLOW_SPIN: polls before a render wave evaluates its window
+    bool flow_force_fallback = false;   // RV_OPT_FLOW_FORCE_FALLBACK (tests): no wave waits, all evaluate
+    bool gi_shard_probe = false;     // RV_OPT_GI_SHARD_PROBE: a sharded loop without a communicator runs its 1/N GI share
     // The next UpdateGIData computed ahead by a flow launch (camera-independent): update `spec_fr` of
     // [spec_first, + spec_count) in gi_tmp, valid while the world/GI version is spec_world; recorded
     // on the launch's stream (ev_spec).  upd_since_frame: an UpdateGIData came since the last frame

@@ -136,9 +136,9 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
     const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
     const int N = tiles ? c->shard_n : 1, R = tiles ? c->shard_rank : 0, T = c->shard_px;
     const bool xchg = tiles && comm;   // GI shard + all-gather, tile gather to rank 0 (also for one rank)
-    // timing probe (env RV_GI_SHARD_PROBE, no communicator): this rank's GI share only, no exchange --
+    // timing probe (RV_OPT_GI_SHARD_PROBE, no communicator): this rank's GI share only, no exchange --
     // the grid is then NOT the reference's; only for sizing the multi-GPU loop on one GPU
-    const bool probe = tiles && !comm && N > 1 && getenv("RV_GI_SHARD_PROBE") != nullptr;
+    const bool probe = tiles && !comm && N > 1 && c->gi_shard_probe;
     const bool shard_gi = xchg || probe;
     const int bpp = c->gather_bpp;
     const size_t slice = tiles ? (size_t)c->shard_max * T * T * bpp : 0;
@@ -285,7 +285,6 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
         // latency-variant launches (a rank's share from 4 ranks, C3) run the GI cells on lane pairs
         const uint32_t rlen = pipe_len(f, PIPE_RENDER, 0);
         p.gi_pairs = (c->gi_pairs > 0 || (c->gi_pairs < 0 && tiles)) && pipe_latency_variant(f, rlen) ? 1u : 0u;
-        p.prio_blocks = c->prio_blocks;
         const uint32_t lens[3] = {more ? pipe_len(f, PIPE_GI, p.gi_pairs ? 2 * mine : mine) : 0u,
                                   more ? pipe_len(f, PIPE_PP, 0) : 0u, rlen};
         for (int i = 0; i < 3; i++) {
@@ -368,8 +367,8 @@ static rv_status render_gi_pipe(rv_ctx* c, const Seq& q, int32_t flags, hipStrea
                 launch_chunk_order(S, c->tile_cost, c->tile_order, (uint32_t)f.ntiles, ((uint32_t)f.ntiles + 7u) & ~7u);
             } else {
                 launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(f.hw, f.hh),
-                                   n_chunks_pad(f.hw, f.hh), chunks_x(f.hw), c->chunk_cost[CG_RENDER],
-                                   c->chunk_order[CG_RENDER], n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H), chunks_x(f.W));
+                                   n_chunks_pad(f.hw, f.hh), c->chunk_cost[CG_RENDER],
+                                   c->chunk_order[CG_RENDER], n_chunks(f.W, f.H), n_chunks_pad(f.W, f.H));
             }
             LAUNCH_CHECK(c);
         }
@@ -421,7 +420,7 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
     const bool tiles = c->shard_n > 0, root = c->shard_rank == 0;
     const int N = tiles ? c->shard_n : 1, R = tiles ? c->shard_rank : 0, T = c->shard_px;
     const bool xchg = tiles && comm;
-    const bool probe = tiles && !comm && N > 1 && getenv("RV_GI_SHARD_PROBE") != nullptr;
+    const bool probe = tiles && !comm && N > 1 && c->gi_shard_probe;
     const bool shard_gi = xchg || probe;
     const int bpp = c->gather_bpp;
     const size_t slice = tiles ? (size_t)c->shard_max * T * T * bpp : 0;
@@ -645,8 +644,8 @@ static rv_status render_gi_group(rv_ctx* c, const Seq& q, int32_t flags, hipStre
                 launch_chunk_order(S, c->tile_cost, c->tile_order, nt, (nt + 7u) & ~7u);
             } else {
                 launch_chunk_order(S, c->chunk_cost[CG_PREPASS], c->chunk_order[CG_PREPASS], n_chunks(fo.hw, fo.hh),
-                                   n_chunks_pad(fo.hw, fo.hh), chunks_x(fo.hw), c->chunk_cost[CG_RENDER],
-                                   c->chunk_order[CG_RENDER], n_chunks(W, H), n_chunks_pad(W, H), chunks_x(W));
+                                   n_chunks_pad(fo.hw, fo.hh), c->chunk_cost[CG_RENDER],
+                                   c->chunk_order[CG_RENDER], n_chunks(W, H), n_chunks_pad(W, H));
             }
             LAUNCH_CHECK(c);
         }
@@ -890,14 +889,7 @@ rv_status rv_set_tile_shard_weighted(rv_ctx* c, int32_t tile_px, int32_t rank, i
 
 rv_status rv_set_tile_shard(rv_ctx* c, int32_t tile_px, int32_t rank, int32_t nranks) {
     if (!c) return RV_ERR_INVALID;
-    float w0 = 1.0f;
-    if (const char* e = getenv("RV_SHARD_ROOT_WEIGHT")) {   // strict: a value that does not parse is an error
-        char* end = nullptr;
-        const double v = strtod(e, &end);
-        if (!end || end == e || *end != '\0') return fail(c, RV_ERR_INVALID, "RV_SHARD_ROOT_WEIGHT does not parse");
-        w0 = (float)v;
-    }
-    return rv_set_tile_shard_weighted(c, tile_px, rank, nranks, w0);
+    return rv_set_tile_shard_weighted(c, tile_px, rank, nranks, 1.0f);
 }
 
 rv_status rv_set_gather_bpp(rv_ctx* c, int32_t bpp) {

@@ -139,7 +139,7 @@ class StateRender:
 
     def __init__(self, log2_dims=(9, 9, 9), width=1920, height=1080, flags=_lib.RV_FLAGS_REFERENCE,
                  atlas=None, device=0, seed=(0, 0), ref_compat=True, ref_oob_jy=0.0,
-                 gi_rays_per_frame=0, gi_init_saturate=False):
+                 gi_rays_per_frame=0, gi_init_saturate=False, tex_table=0, exits_off=0):
         self._L = _lib.load()
         self.width, self.height = int(width), int(height)
         self.log2_dims = tuple(int(v) for v in log2_dims)
@@ -155,6 +155,7 @@ class StateRender:
             cfg.atlas_h, cfg.atlas_w = self._atlas.shape[0], self._atlas.shape[1]
         cfg.gi_rays_per_frame = int(gi_rays_per_frame)
         cfg.gi_init_saturate = int(bool(gi_init_saturate))
+        cfg.tex_table, cfg.exits_off = int(tex_table), int(exits_off)
         h = C.c_void_p()
         st = self._L.rv_create(C.byref(cfg), int(device), C.byref(h))
         if st != 0:
@@ -181,6 +182,15 @@ class StateRender:
             self.close()
         except Exception:
             pass
+
+    def set_option(self, option, value):
+        """rv_set_option (include/rvgrt.h): RV_OPT_* run-time options."""
+        self._check(self._L.rv_set_option(self._h, int(option), int(value)), "rv_set_option")
+
+    def get_option(self, option) -> int:
+        v = C.c_int64()
+        self._check(self._L.rv_get_option(self._h, int(option), C.byref(v)), "rv_get_option")
+        return int(v.value)
 
     def set_stream(self, stream_handle: int):
         self._check(self._L.rv_set_stream(self._h, C.c_void_p(stream_handle)), "rv_set_stream")
@@ -300,7 +310,7 @@ class StateRender:
 
     def set_tile_shard(self, tile_px, rank, nranks, root_weight=None):
         """This rank's interleaved share of T x T tiles for render_frames (0 ranks = full frames);
-        root_weight = rank 0's share relative to the others (default: env RV_SHARD_ROOT_WEIGHT or 1)."""
+        root_weight = rank 0's share relative to the others (default 1)."""
         if root_weight is None:
             self._check(self._L.rv_set_tile_shard(self._h, int(tile_px), int(rank), int(nranks)), "rv_set_tile_shard")
         else:

@@ -127,9 +127,9 @@ void world_dtop(HostWorld& h) {
         }
 }
 
-template <int G, bool REUSE, bool RW = true, int SPEC = 0>
+template <int G, bool REUSE, bool RW = true>
 Hit trace_v(const World& w, f3 o, f3 d, float t, StepCount& sc) {
-    return trace<true, G, REUSE, RW, false, World, false, SPEC>(w, o, d, t, sc);
+    return trace<true, G, REUSE, RW, false, World, false>(w, o, d, t, sc);
 }
 }  // namespace
 
@@ -139,9 +139,8 @@ extern "C" {
 struct HostHit { float pos[3], normal[3], u, v; int32_t hit, undef, sphere, dda, check, pad; };
 
 // variant: 0..3 = DDA look-ahead group 1/2/4/8 (stop search + re-walk), 4 = group 1 with word
-// reuse, 5..6 = group 4 / 8 with the step-by-step replay (trace RW = false), 7..8 = group 8 with
-// speculative sphere steps (SPEC 1 / 3), 9 = group 4 with SPEC 3
-int rvh_variants(void) { return 10; }
+// reuse, 5..6 = group 4 / 8 with the step-by-step replay (trace RW = false)
+int rvh_variants(void) { return 7; }
 
 // rv::u8f, the device's byte -> float conversion
 float rvh_u8f(uint32_t b) { return rv::u8f(b); }
@@ -201,10 +200,9 @@ int rvh_trace_rays_sky_exit(int variant, int lx, int ly, int lz, const uint32_t*
 
 // Rays toward the sun through trace_sun with the sky exit and the sun horizon built for `sun`
 // (every direction must be exactly `sun`, as for the kernels' shadow rays); hz_out: the horizon map.
-// g8: bit 0 = look-ahead 8 (else 4); bits 1-2 = speculative sphere steps (0, 1 or 3)
+// g8: 1 = look-ahead 8 (else 4)
 int rvh_trace_sun(int g8, int lx, int ly, int lz, const uint32_t* bits, const uint8_t* csdf, const float* sun,
                   const float* org, const float* dist, int64_t n, HostHit* out, uint32_t* hz_out) {
-    const int spec = (g8 >> 1) & 3;
     g8 &= 1;
     HostWorld h;
     build(h, lx, ly, lz, bits, csdf);
@@ -216,10 +214,7 @@ int rvh_trace_sun(int g8, int lx, int ly, int lz, const uint32_t* bits, const ui
     for (int64_t i = 0; i < n; i++) {
         StepCount sc{};
         const f3 o = V(org[3 * i], org[3 * i + 1], org[3 * i + 2]);
-        constexpr bool CS = (RV_COL_SUN != 0) && (RV_DDA_REWALK != 0);
-        Hit r = spec == 1 ? trace_sun<true, 8, false, World, CS, 1>(h.w, o, d, hround(dist[i]), sc)
-              : spec == 3 ? trace_sun<true, 8, false, World, CS, 3>(h.w, o, d, hround(dist[i]), sc)
-              : g8 ? trace_sun<true, 8, false>(h.w, o, d, hround(dist[i]), sc)
+        Hit r = g8 ? trace_sun<true, 8, false>(h.w, o, d, hround(dist[i]), sc)
                    : trace_sun<true, 4, false>(h.w, o, d, hround(dist[i]), sc);
         HostHit& q = out[i];
         q.pos[0] = r.pos.x; q.pos[1] = r.pos.y; q.pos[2] = r.pos.z;
@@ -269,9 +264,6 @@ static int trace_rays(int variant, int lx, int ly, int lz, const uint32_t* bits,
     case 4: fn = trace_v<1, true>; break;
     case 5: fn = trace_v<4, false, false>; break;
     case 6: fn = trace_v<8, false, false>; break;
-    case 7: fn = trace_v<8, false, true, 1>; break;
-    case 8: fn = trace_v<8, false, true, 3>; break;
-    case 9: fn = trace_v<4, false, true, 3>; break;
     default: return -1;
     }
     HostWorld h;

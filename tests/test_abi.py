@@ -31,7 +31,8 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_struct_sizes():
     from rvgrt_amd import _lib
     L = _lib.load()
-    assert L.rv_abi_version() == 1
+    assert L.rv_abi_version() == 2   # 2: gi_init_saturate, tex_table, exits_off, rv_set_option
+    assert C.sizeof(_lib.rv_config) == 72       # the C layout of include/rvgrt.h (pointer at offset 40)
     assert C.sizeof(_lib.rv_hit) == 56          # 8 floats + 6 int32
     assert C.sizeof(_lib.rv_stats) == 16 * 8
     assert C.sizeof(_lib.rv_camera) == 16 * 4

@@ -1,0 +1,61 @@
+"""bench.py's multi-GPU contract on the CPU: `--gpus N` is honoured with and
+without a launcher.  --rehearse runs the rank plumbing
+only (gloo process group, barrier-bracketed timing, max over ranks, rank 0's
+single JSON line) -- the GPU path is exercised by the driver's runs."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(kw)
+    return env
+
+
+def _run(args, env, timeout=240):
+    return subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_without_launcher_spawns_n_ranks(n):
+    p = _run(["--gpus", str(n), "--rehearse", "--steps", "4", "--warmup", "0", "--dist-backend", "gloo"], _env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["ranks_timed"] == n and rec["rehearsal"] is True
+
+
+@pytest.mark.timeout(120)
+def test_launcher_world_size_must_match_gpus():
+    p = _run(["--gpus", "2", "--rehearse"], _env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert p.returncode != 0
+    assert "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.timeout(120)
+def test_one_gpu_rehearsal_single_rank():
+    p = _run(["--rehearse", "--steps", "2"], _env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 1
+
+
+@pytest.mark.timeout(300)
+def test_under_torch_distributed_run():
+    """The driver's launcher form: torch.distributed.run with --nproc-per-node N and --gpus N."""
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29613", BENCH, "--gpus", "2", "--rehearse",
+                        "--steps", "3"], env=_env(), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(recs) == 1 and recs[0]["n_gpus"] == 2

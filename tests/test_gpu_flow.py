@@ -52,13 +52,15 @@ def test_flow_frames_equal_two_launches_and_oracle(rv, atlas, oracle, monkeypatc
     behind each other); the grid equals the oracle's rolling updates and the
     last frame the oracle's render (RGBA8, MV, depth); no render wave had to
     fall back to evaluating its own window.  pairs: the GI cells of these (latency-variant) launches on
-    lane pairs (RV_GI_PAIRS)."""
+    lane pairs (RV_OPT_GI_PAIRS)."""
     from rvgrt_amd.configs import TEST_POSES_128, camera_path
-    monkeypatch.setenv("RV_GI_PAIRS", str(pairs))
     lg, W, H = 7, 320, 192
     nfr = 11
     seq = camera_path(TEST_POSES_128[pose], W, H, nfr + 1, pan=0.02, ref_compat=True)
     a, b = _make(rv, atlas, lg, W, H, rays, 1), _make(rv, atlas, lg, W, H, rays, 0)
+    for r in (a, b):
+        r.set_option(rv.RV_OPT_GI_PAIRS, pairs)
+        assert r.get_option(rv.RV_OPT_GI_PAIRS) == pairs
     for k in range(nfr):
         for r in (a, b):
             r.update_gi_data()
@@ -122,17 +124,17 @@ def test_flow_gi_computed_ahead_is_dropped_when_stale(rv, atlas):
 
 
 def test_flow_fallback_evaluates_the_same_texels(rv, atlas, monkeypatch):
-    """The bounded wait's way out: with RV_FLOW_FORCE_FALLBACK every render
+    """The bounded wait's way out: with RV_OPT_FLOW_FORCE_FALLBACK every render
     wave waits for a value no pre-pass wave publishes, gives up after
-    RV_FLOW_SPIN polls and evaluates its half-res window itself -- the frames
-    must not change (and every render wave is counted)."""
+    RV_OPT_FLOW_SPIN polls and evaluates its half-res window itself (distance
+    and shadow) -- the frames must not change (and every render wave is counted)."""
     from rvgrt_amd.configs import TEST_POSES_128, camera_path
     lg, W, H, rays = 7, 160, 96, 5000
     seq = camera_path(TEST_POSES_128["P1"], W, H, 4, pan=0.02, ref_compat=True)
     b = _make(rv, atlas, lg, W, H, rays, 0)
-    monkeypatch.setenv("RV_FLOW_FORCE_FALLBACK", "1")
-    monkeypatch.setenv("RV_FLOW_SPIN", "4")
     a = _make(rv, atlas, lg, W, H, rays, 1)
+    a.set_option(rv.RV_OPT_FLOW_FORCE_FALLBACK, 1)
+    a.set_option(rv.RV_OPT_FLOW_SPIN, 4)
     for k in range(3):
         for r in (a, b):
             r.update_gi_data()
@@ -175,9 +177,9 @@ def test_flow_fallback_throughput_variant_4k(rv, atlas, monkeypatch):
     lg, W, H, rays = 8, 3840, 2160, 5000
     seq = camera_path(pose_f32(CONFIGS["c1"], "P0"), W, H, 3, pan=0.01, ref_compat=True)
     b = _make(rv, atlas, lg, W, H, rays, 0)
-    monkeypatch.setenv("RV_FLOW_FORCE_FALLBACK", "1")
-    monkeypatch.setenv("RV_FLOW_SPIN", "2")
     a = _make(rv, atlas, lg, W, H, rays, 1)
+    a.set_option(rv.RV_OPT_FLOW_FORCE_FALLBACK, 1)
+    a.set_option(rv.RV_OPT_FLOW_SPIN, 2)
     for k in range(2):
         for r in (a, b):
             r.update_gi_data()

@@ -40,11 +40,11 @@ def test_grouped_frames_equal_one_at_a_time(rv, atlas, oracle, monkeypatch, F, r
     calls of 1, 2, 5, 7 and 3 frames on a moving camera, so groups end
     mid-call and calls end mid-group."""
     from rvgrt_amd.configs import TEST_POSES_128, camera_path
-    monkeypatch.setenv("RV_PIPE_ORDER", order)
     lg, W, H = 7, 320, 192
     flags = rv.RV_FLAGS_REFERENCE
     seq = camera_path(TEST_POSES_128["P0"], W, H, 18, pan=0.01, ref_compat=True)
     ref, r = _make(rv, atlas, lg, W, H, rays), _make(rv, atlas, lg, W, H, rays)
+    r.set_option(rv.RV_OPT_PIPE_ORDER, int(order, 16))
     ref.set_pipeline(0)
     r.set_frame_group(F)
     k = 0

@@ -206,16 +206,15 @@ def test_loopback_ranks_full_size(rv, atlas, monkeypatch, cfgname, N, w0, grp):
     grid equal to one context rendering UpdateGIData + drawCUDA one frame at a time.  Full-size shares
     exercise what the 128^3 cases cannot: 2,040 tiles with padded weighted slices, 16-frame groups
     carrying whole-size GI windows, 33 MB RGB24 gather buffers.  C5's ranks run without the texture
-    tile table (32 GiB each at 2048^3; the tiles are the same either way)."""
+    tile table (7.25 GB each at 2048^3, nine contexts on one GPU; the tiles are the same either way)."""
     from rvgrt_amd.configs import CONFIGS, camera_path, pose_f32
     cfg = CONFIGS[cfgname]
-    if cfgname == "c5":
-        monkeypatch.setenv("RV_TEX_TABLE", "0")
     W, H = cfg.width, cfg.height
     seq = camera_path(pose_f32(cfg, "P0"), W, H, 21, pan=0.0005, ref_compat=True)
 
     def make():
-        r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=atlas)
+        r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=atlas,
+                           tex_table=-1 if cfgname == "c5" else 0)
         r.world_build()
         for s in range(cfg.gi_sweeps):
             r.gi_update(s)

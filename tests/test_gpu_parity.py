@@ -457,16 +457,16 @@ def test_pipelined_reference_frames(rv, atlas, oracle, monkeypatch, order, rays,
     that wraps (5000-cell windows of a 32^3 grid: linear cell order, a partial
     last block; 4096 / 2048: whole planes, blocked cell order) -- and the
     oracle agrees on the grid (bit-exact) and the last frame.  pairs: the latency variant's GI cells on
-    lane pairs (RV_GI_PAIRS; this small frame's launches are latency-variant ones)."""
+    lane pairs (RV_OPT_GI_PAIRS; this small frame's launches are latency-variant ones)."""
     from rvgrt_amd.configs import TEST_POSES_128
-    monkeypatch.setenv("RV_PIPE_ORDER", order)
-    monkeypatch.setenv("RV_GI_PAIRS", str(pairs))
     lg, W, H = 7, 320, 192
     flags = rv.RV_FLAGS_REFERENCE
     cam, vp = rv.camera_from_pose(*TEST_POSES_128["P0"], W, H)
 
     def make():
         r = rv.StateRender((lg, lg, lg), W, H, flags=flags, atlas=atlas, gi_rays_per_frame=rays)
+        r.set_option(rv.RV_OPT_PIPE_ORDER, int(order, 16))
+        r.set_option(rv.RV_OPT_GI_PAIRS, pairs)
         r.world_build()
         r.gi_update(0)
         return r
@@ -516,17 +516,17 @@ def test_pipelined_frames_stats(rv, atlas):
 
 
 def test_render_frames_two_streams(rv, atlas, monkeypatch):
-    """RV_BATCH_STREAMS=2 (what bench.py uses with N > 1): groups alternate over
+    """RV_OPT_BATCH_STREAMS = 2 (what bench.py uses with N > 1): groups alternate over
     two streams so one group's tail overlaps the next; frames must not change --
     whole frames, a one-rank shard and the one-rank RCCL gather path."""
     from rvgrt_amd.configs import TEST_POSES_128
-    monkeypatch.setenv("RV_BATCH_STREAMS", "2")
     lg, W, H, T = 7, 320, 192, 16
     ref = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=8, gi_sweeps=1)
     cam, vp = rv.camera_from_pose(*TEST_POSES_128["P1"], W, H)
     ref.frame(cam, vp)
     want = ref.readback(rv.RV_IMAGE_COLOR).copy()
     r = _gpu_world(rv, atlas, lg, lg, lg, W, H, flags=8, gi_sweeps=1)
+    r.set_option(rv.RV_OPT_BATCH_STREAMS, 2)
     r.set_frames_in_flight(4)
     r.render_frames(11, cam, vp)
     assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), want)

@@ -4,7 +4,7 @@ The table is built once per context, for the world of its first build or bits im
 rows below that world's sky exit; it is kept through later world writes.  A later world that rises
 above those rows must still render exactly: its hits above the table's rows take sampleTexture's noise
 (src/raytracing_functions.cu:41-54), as hits outside the world do.  Checked against a context without
-the table (RV_TEX_TABLE=0), which evaluates the noise for every hit.
+the table (rv_config.tex_table = -1), which evaluates the noise for every hit.
 """
 import numpy as np
 import pytest
@@ -34,11 +34,8 @@ def test_rows_above_the_table_take_the_noise(rv, atlas, oracle_world, monkeypatc
     W, H = 192, 128
 
     def context(table):
-        if not table:
-            monkeypatch.setenv("RV_TEX_TABLE", "0")
-        r = rv.StateRender((7, 7, 7), W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+        r = rv.StateRender((7, 7, 7), W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas, tex_table=0 if table else -1)
         r.world_import(rv.RV_WORLD_BITS, _bits(low))   # the table's world
-        monkeypatch.delenv("RV_TEX_TABLE", raising=False)
         return r
 
     def frames(r, vox):

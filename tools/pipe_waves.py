@@ -29,6 +29,8 @@ def main():
     torch.cuda.set_device(0)
     W, H = cfg.width, cfg.height
     r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=load_atlas())
+    if os.environ.get("RV_GI_SHARD_PROBE"):   # this tool's knob -> the library option
+        r.set_option(rv.RV_OPT_GI_SHARD_PROBE, 1)
     r.world_build()
     for s in range(max(cfg.gi_sweeps, 0)):
         r.gi_update(s)

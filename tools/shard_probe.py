@@ -45,6 +45,11 @@ def main():
     torch.cuda.set_device(0)
     W, H = cfg.width, cfg.height
     r = rv.StateRender((cfg.log2_n,) * 3, W, H, flags=cfg.flags, atlas=load_atlas())
+    # the tool's own knobs (tools/measure.sh): run-time options of the library (include/rvgrt.h rv_option)
+    if os.environ.get("RV_GI_SHARD_PROBE"):
+        r.set_option(rv.RV_OPT_GI_SHARD_PROBE, 1)
+    if os.environ.get("RV_PIPE_ORDER"):
+        r.set_option(rv.RV_OPT_PIPE_ORDER, int(os.environ["RV_PIPE_ORDER"], 16))
     r.world_build()
     for s in range(max(cfg.gi_sweeps, 0)):
         r.gi_update(s)
