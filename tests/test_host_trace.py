@@ -23,10 +23,13 @@ HIT = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("u", "<f4"), ("v", "<f
 VARIANTS = {"g1": 0, "g2": 1, "g4": 2, "g8": 3, "g1_reuse": 4, "g4_replay": 5, "g8_replay": 6}
 
 
+SAN = os.environ.get("RVGRT_SANITIZE") == "1"   # tests/test_sanitizers.py: the ASan + UBSan build
+
+
 @pytest.fixture(scope="module")
 def host_lib():
-    subprocess.run(["make", "-s", "-C", HOST], check=True)
-    L = C.CDLL(os.path.join(HOST, "build", "librvhost.so"))
+    subprocess.run(["make", "-s", "-C", HOST] + (["san"] if SAN else []), check=True)
+    L = C.CDLL(os.path.join(HOST, "build", "librvhost_san.so" if SAN else "librvhost.so"))
     L.rvh_trace_rays.restype = C.c_int
     L.rvh_trace_rays.argtypes = [C.c_int] * 4 + [C.c_void_p] * 5 + [C.c_int64, C.c_void_p]
     assert L.rvh_variants() == len(VARIANTS)
