@@ -11,7 +11,10 @@ they ran; and the pre-pass tiles of the longest waves, with the RV_FLOW_OPTS val
 wave alone (4: no GI or render part, 8: one pre-pass tile) -- its chain on an idle chip.  Not part of
 the product.
 
-usage: python tools/flow_waves.py [config] [pose] [frames]
+usage: python tools/flow_waves.py [config] [pose] [frames] [--no-gi]
+  --no-gi: renderLoop without its UpdateGIData calls, so the flow launches hold no GI window (an ablation:
+           pre-pass + render).  Every run also prints the mean k_ref_flow launch time over its frames (HIP
+           events, after 8 warm-up frames) as MEAN_LAUNCH_US.
 """
 import os
 import sys
@@ -33,9 +36,11 @@ def main():
     from rvgrt_amd.atlas import load_atlas
     from rvgrt_amd.configs import CONFIGS, camera_path, pose_f32
 
-    cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c3"]
-    pose = sys.argv[2] if len(sys.argv) > 2 else "P0"
-    nfr = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+    argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+    no_gi = "--no-gi" in sys.argv
+    cfg = CONFIGS[argv[0] if len(argv) > 0 else "c3"]
+    pose = argv[1] if len(argv) > 1 else "P0"
+    nfr = int(argv[2]) if len(argv) > 2 else 40
     path = os.path.join(tempfile.gettempdir(), f"flow_waves_{os.getpid()}.bin")
     os.environ["RV_FLOW_WAVE_TRACE"] = path
     torch.cuda.set_device(0)
@@ -46,12 +51,19 @@ def main():
         r.gi_update(s)
     seq = camera_path(pose_f32(cfg, pose), W, H, nfr, pan=0.0005, ref_compat=True)
     for k in range(nfr):
+        if k == 8:
+            r.sync()
+            r.timing_enable(2 * nfr + 2)
         d = seq[k]
         c = d.cam
-        r.update_gi_data()
+        if not no_gi:
+            r.update_gi_data()
         r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(d.vp),
                     np.ctypeslib.as_array(d.prev_vp), 0.0, d.time)
     r.sync()
+    ms, _ = r.timing_stages()
+    nl = r.timing_launches()
+    mean_us = 1000.0 * ms["primary"] / nl["primary"] if nl["primary"] else 0.0
     r.close()
     raw = np.fromfile(path, np.uint32)
     os.unlink(path)
@@ -67,7 +79,9 @@ def main():
     tile = rec[:, 0] >> 8                   # pre-pass waves: bx | by << 12 (diagnostics builds)
     names = {1: "prepass", 0: "gi", 2: "render"}
     print(f"{cfg.name} {pose}: {W}x{H}, workgroups pre-pass {lens[0]}, GI {lens[1]}, render {lens[2]}; "
-          f"launch span {end.max():.1f} us")
+          f"launch span {end.max():.1f} us (last launch)")
+    print(f"MEAN_LAUNCH_US {mean_us:.1f} over {nl['primary']} launches (RV_FLOW_OPTS={os.environ.get('RV_FLOW_OPTS', '0')}"
+          f"{', no GI window' if no_gi else ''})")
     for q in (1, 0, 2):
         m = part == q
         if not m.any():

@@ -141,6 +141,20 @@ tile-alone)
     RV_FLOW_OPTS=$opts run fw_tile 200 python tools/flow_waves.py "$c" "$pose" "$n"
     grep -h "launch span\|life\|longest pre-pass" "gpurun_out/${TAG}_fw_full.log" "gpurun_out/${TAG}_fw_alone.log" \
         "gpurun_out/${TAG}_fw_tile.log" ;;
+flow-ablation)
+    # the drop-in flow launch itemised: full | pre-pass + render (no GI window) | pre-pass +
+    # GI window (render exits) | pre-pass alone | the longest pre-pass tile alone on an idle chip
+    c=${1:-c3}; pose=${2:-P0}; n=${3:-60}
+    export RVGRT_LIB=rvgrt_amd/variants/diag/librvgrt_hip.so
+    run fa_full 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    run fa_nogi 200 python tools/flow_waves.py "$c" "$pose" "$n" --no-gi
+    RV_FLOW_OPTS=16 run fa_ppgi 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    RV_FLOW_OPTS=4 run fa_pp 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    opts=$(grep LONGEST_TILE_OPTS "gpurun_out/${TAG}_fa_full.log" | awk '{print $2}')
+    RV_FLOW_OPTS=$opts run fa_tile 200 python tools/flow_waves.py "$c" "$pose" "$n"
+    for m in full nogi ppgi pp tile; do
+        echo "== $m"; grep -h "MEAN_LAUNCH\|launch span\|life\|wait\|run \|longest pre-pass\|done at" "gpurun_out/${TAG}_fa_$m.log"
+    done ;;
 *)
-    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard|shard-orders|pmc-l1|tile-alone ..."; exit 2 ;;
+    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard|shard-orders|pmc-l1|tile-alone|flow-ablation ..."; exit 2 ;;
 esac
