@@ -40,9 +40,6 @@
 #ifndef RV_COL_GI         // ... the GI update's bounce rays too (A/B)
 #define RV_COL_GI 0
 #endif
-#ifndef RV_WATER_PK       // the water normal's two fbm3D evaluated two-wide (rv_device.h fbm3D_2)
-#define RV_WATER_PK 1
-#endif
 #ifndef RV_G_GI           // GI init / update
 #define RV_G_GI 4
 #endif
@@ -195,14 +192,8 @@ __device__ __forceinline__ f3 compute_color(const WV& w, const FrameParams& f, f
     if (STATS) { c[CNT_TRACES]++; c[CNT_PRIMARY]++; c[CNT_UNDEF] += hit.undef; }
     f3 color;
     if (hit.hit && hit.pos.y < 31.001f && has<FEAT>(f, RV_F_WATER)) {
-#if RV_WATER_PK   // the two fbm3D as one two-wide evaluation (packed float math, bit-identical)
-        const f2v nw = fbm3D_2(f2v{hit.pos.x, hit.pos.z}, f2v{hit.pos.z, hit.pos.x}, f2v{f.time, f.time + 112.0f}, 3,
-                               0.06f, 2.0f, 0.6f);
-        const float nxw = nw.x, nyw = nw.y;
-#else
         float nxw = fbm3D(hit.pos.x, hit.pos.z, f.time, 3, 0.06f, 2.0f, 0.6f);
         float nyw = fbm3D(hit.pos.z, hit.pos.x, f.time + 112.0f, 3, 0.06f, 2.0f, 0.6f);
-#endif
         f3 dn = normalize(add(hit.normal, V(nxw * 0.1f, nyw * 0.1f, 0.0f)));
         f3 rdir = reflect(dir, dn);
         RV_GD_KIND(gd::REFL);

@@ -150,17 +150,6 @@ void rvh_simplex3D(const float* xyz, float* out, int64_t n) {
     for (int64_t i = 0; i < n; i++) out[i] = rv::simplex3D(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
 }
 
-// the water normal's noise pair: fbm3D_2 of (x, z, t) and (z, x, t + 112) against two scalar fbm3D
-void rvh_water_noise(const float* xzt, float* pair, float* scalar, int64_t n) {
-    for (int64_t i = 0; i < n; i++) {
-        const float x = xzt[3 * i], z = xzt[3 * i + 1], t = xzt[3 * i + 2];
-        const f2v r = fbm3D_2(f2v{x, z}, f2v{z, x}, f2v{t, t + 112.0f}, 3, 0.06f, 2.0f, 0.6f);
-        pair[2 * i] = r.x; pair[2 * i + 1] = r.y;
-        scalar[2 * i] = fbm3D(x, z, t, 3, 0.06f, 2.0f, 0.6f);
-        scalar[2 * i + 1] = fbm3D(z, x, t + 112.0f, 3, 0.06f, 2.0f, 0.6f);
-    }
-}
-
 // sampleTexture's tile (0xYX) for n positions in a 2^lx x 2^ly x 2^lz world, through the World::tex
 // table (built on the host with k_tex_table's element function) and through the noise (tex = null)
 // ny: the rows the table covers (0: all; else a multiple of 8, the band below the sky exit)

@@ -268,22 +268,3 @@ def test_column_skip_keeps_every_hit(host_lib, g8):
     assert b["pad"].sum() == 0 and skipped > 0.05 * groups.sum(), (skipped, groups.sum())
     desc = d[:, 1] < 0
     assert a["pad"][desc].sum() > 0 and a["pad"][~desc].sum() > 0   # both branches of the row bound fire
-
-
-def test_noise_pair_equals_scalar(host_lib):
-    """rv_device.h fbm3D_2 (the water normal's two fbm3D evaluated two-wide, packed float math on the GPU)
-    equals two scalar fbm3D bit for bit: water-plane positions, large coordinates, negative ones, lattice
-    points and the times the bench's camera path uses."""
-    rng = np.random.default_rng(11)
-    n = 200000
-    xzt = np.empty((n, 3), np.float32)
-    xzt[:, :2] = rng.uniform(-5000, 5000, (n, 2))
-    xzt[: n // 4, :2] = np.round(xzt[: n // 4, :2])              # lattice points
-    xzt[n // 4: n // 2, :2] = rng.uniform(0, 2048, (n // 4, 2))    # inside the worlds
-    xzt[:, 2] = rng.choice(np.array([0.0, 0.125, -0.0625, 0.4375, 37.5, 1e4], np.float32), n)
-    pair = np.zeros((n, 2), np.float32)
-    scal = np.zeros((n, 2), np.float32)
-    host_lib.rvh_water_noise.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
-    host_lib.rvh_water_noise(xzt.ctypes.data, pair.ctypes.data, scal.ctypes.data, n)
-    assert np.array_equal(pair.view(np.uint32), scal.view(np.uint32))
-    assert np.abs(scal).max() > 0.1
