@@ -11,9 +11,11 @@ they ran; and the pre-pass tiles of the longest waves, with the RV_FLOW_OPTS val
 wave alone (4: no GI or render part, 8: one pre-pass tile) -- its chain on an idle chip.  Not part of
 the product.
 
-usage: python tools/flow_waves.py [config] [pose] [frames] [--no-gi]
+usage: python tools/flow_waves.py [config] [pose] [frames] [--no-gi] [--static]
   --no-gi: renderLoop without its UpdateGIData calls, so the flow launches hold no GI window (an ablation:
-           pre-pass + render).  Every run also prints the mean k_ref_flow launch time over its frames (HIP
+           pre-pass + render).
+  --static: every frame takes the first frame's camera (the same rays each launch: with one pre-pass tile
+           alone, its chain runs on the caches the previous launch left, against a 1-frame run's cold one).  Every run also prints the mean k_ref_flow launch time over its frames (HIP
            events, after 8 warm-up frames) as MEAN_LAUNCH_US.
 """
 import os
@@ -38,6 +40,7 @@ def main():
 
     argv = [a for a in sys.argv[1:] if not a.startswith("--")]
     no_gi = "--no-gi" in sys.argv
+    static = "--static" in sys.argv
     cfg = CONFIGS[argv[0] if len(argv) > 0 else "c3"]
     pose = argv[1] if len(argv) > 1 else "P0"
     nfr = int(argv[2]) if len(argv) > 2 else 40
@@ -54,12 +57,12 @@ def main():
         if k == 8:
             r.sync()
             r.timing_enable(2 * nfr + 2)
-        d = seq[k]
+        d = seq[0] if static else seq[k]
         c = d.cam
         if not no_gi:
             r.update_gi_data()
         r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(d.vp),
-                    np.ctypeslib.as_array(d.prev_vp), 0.0, d.time)
+                    np.ctypeslib.as_array(d.vp if static else d.prev_vp), 0.0, d.time)
     r.sync()
     ms, _ = r.timing_stages()
     nl = r.timing_launches()
@@ -81,7 +84,7 @@ def main():
     print(f"{cfg.name} {pose}: {W}x{H}, workgroups pre-pass {lens[0]}, GI {lens[1]}, render {lens[2]}; "
           f"launch span {end.max():.1f} us (last launch)")
     print(f"MEAN_LAUNCH_US {mean_us:.1f} over {nl['primary']} launches (RV_FLOW_OPTS={os.environ.get('RV_FLOW_OPTS', '0')}"
-          f"{', no GI window' if no_gi else ''})")
+          f"{', no GI window' if no_gi else ''}{', static camera' if static else ''})")
     for q in (1, 0, 2):
         m = part == q
         if not m.any():

@@ -155,6 +155,19 @@ flow-ablation)
     for m in full nogi ppgi pp tile; do
         echo "== $m"; grep -h "MEAN_LAUNCH\|launch span\|life\|wait\|run \|longest pre-pass\|done at" "gpurun_out/${TAG}_fa_$m.log"
     done ;;
+tile-warm)
+    # is the longest pre-pass chain memory-latency bound?  The same frame every launch (static camera): the
+    # longest tile alone after a 1-frame run (caches hold the world build's lines) against after 20 launches
+    # of that tile (its own lines left in L2 / MALL by the previous launch)
+    c=${1:-c3}; pose=${2:-P0}
+    export RVGRT_LIB=rvgrt_amd/variants/diag/librvgrt_hip.so
+    run tw_full 200 python tools/flow_waves.py "$c" "$pose" 20 --static
+    opts=$(grep LONGEST_TILE_OPTS "gpurun_out/${TAG}_tw_full.log" | awk '{print $2}')
+    RV_FLOW_OPTS=$opts run tw_cold 200 python tools/flow_waves.py "$c" "$pose" 1 --static
+    RV_FLOW_OPTS=$opts run tw_warm 200 python tools/flow_waves.py "$c" "$pose" 20 --static
+    for m in full cold warm; do
+        echo "== $m"; grep -h "MEAN_LAUNCH\|launch span\|longest pre-pass\|done at" "gpurun_out/${TAG}_tw_$m.log"
+    done ;;
 *)
-    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard|shard-orders|pmc-l1|tile-alone|flow-ablation ..."; exit 2 ;;
+    echo "usage: tools/measure.sh tests|bench|pmc|prof|ab|shard|shard-orders|pmc-l1|tile-alone|flow-ablation|tile-warm ..."; exit 2 ;;
 esac
