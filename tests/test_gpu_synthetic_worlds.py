@@ -1,0 +1,174 @@
+"""GPU parity on worlds the terrain generator never makes: imported voxel bits
+(rv_world_import) with the CSDF and the GI grid built on the GPU from them, against
+the oracle building the same from the same bits.
+
+The procedural worlds of the other tests are smooth height fields with a solid
+floor; these reach the traversal's remaining paths: rays that start inside solid
+voxels (the reference's mask = -128 hit, Appendix R2) on every pixel of a full
+world, an empty world (every ray leaves the grid; no sky row, no sun horizon),
+1 to 40 % random occupancy (DDA stops at every distance, CSDF values 0-64 in every
+cell), one-voxel pillars (grazing rays along faces, the column skip between them)
+and ragged power-of-two dims.  Bar: bit-exact -- CSDF, GI init, a GI update window,
+20,000 traced rays with the reference's step counts, and whole frames (RGBA8,
+motion, depth, half-res distance) at the reference's flags and the C2 flags.
+"""
+import numpy as np
+import pytest
+
+from conftest import random_rays
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rv():
+    import rvgrt_amd
+    rvgrt_amd._lib.load()
+    return rvgrt_amd
+
+
+def _voxels(kind, X, Y, Z, rng):
+    """Dense [z, y, x] occupancy of one synthetic world."""
+    if kind == "empty":
+        return np.zeros((Z, Y, X), bool)
+    if kind == "full":
+        return np.ones((Z, Y, X), bool)
+    if kind == "sparse":
+        return rng.uniform(size=(Z, Y, X)) < 0.01
+    if kind == "dense":
+        return rng.uniform(size=(Z, Y, X)) < 0.40
+    if kind == "pillars":            # a floor and 1-voxel pillars of mixed heights every 6 voxels
+        v = np.zeros((Z, Y, X), bool)
+        v[:, :8, :] = True
+        h = rng.integers(10, Y - 10, (Z // 6 + 1, X // 6 + 1))
+        for k in range(0, Z, 6):
+            for i in range(0, X, 6):
+                v[k, :h[k // 6, i // 6], i] = True
+        return v
+    if kind == "blocks":             # 4^3 blocks at 10 %, with a floor (ragged dims)
+        b = rng.uniform(size=(Z // 4, Y // 4, X // 4)) < 0.10
+        v = b.repeat(4, 0).repeat(4, 1).repeat(4, 2)
+        v[:, :2, :] = True
+        return v
+    raise ValueError(kind)
+
+
+WORLDS = [("empty", (7, 7, 7)), ("full", (6, 6, 6)), ("sparse", (7, 7, 7)), ("dense", (6, 6, 6)),
+          ("pillars", (7, 7, 7)), ("blocks", (6, 5, 7))]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kind,dims", WORLDS, ids=[w[0] for w in WORLDS])
+def test_synthetic_world_bit_exact(rv, atlas, oracle, kind, dims):
+    lx, ly, lz = dims
+    ow = oracle.OracleWorld(lx, ly, lz, atlas=atlas)
+    X, Y, Z = ow.X, ow.Y, ow.Z
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    vox = _voxels(kind, X, Y, Z, rng)
+    ow.bits[:] = np.packbits(vox.ravel(), bitorder="little").view(np.uint32)
+    ow.build_csdf()
+    ow.gi_init()
+
+    W, H = 160, 96
+    r = rv.StateRender(dims, W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+    try:
+        r.world_import(rv.RV_WORLD_BITS, ow.bits)
+        r.csdf_build()
+        assert np.array_equal(r.world_export(rv.RV_WORLD_CSDF), ow.csdf), "CSDF built from the imported bits"
+        r.gi_init()
+        assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi), "GI init"
+        n = len(ow.gi) // 4
+        first, count = n // 5, min(n - n // 5, 9000)
+        r.gi_update(2, first=first, count=count)
+        ow.gi_update(2, first=first, count=count)
+        assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi), "GI update window"
+
+        org, d, dist = random_rays(np.random.default_rng(7), 20000, (X, Y, Z))
+        g = r.trace_rays(org, d, dist)
+        o = ow.trace_batch(org, d, dist)
+        assert (g["hit"] == o["hit"]).all() and (g["undef"] == o["undef"]).all()
+        assert np.array_equal(g["pos"].view(np.uint32), o["pos"].view(np.uint32))
+        assert np.array_equal(g["normal"], o["normal"])
+        assert np.array_equal(g["u"].view(np.uint32), o["u"].view(np.uint32))
+        assert np.array_equal(g["v"].view(np.uint32), o["v"].view(np.uint32))
+        for a, b in (("sphere_steps", "n_sphere"), ("dda_steps", "n_dda"), ("csdf_checks", "n_check")):
+            assert np.array_equal(g[a], o[b]), a
+        if kind == "empty":
+            assert not o["hit"].any()
+        if kind == "full":   # every ray that starts in the grid starts in a solid voxel (R2)
+            p0 = org + d * dist[:, None]
+            inside = ((p0 >= 0) & (p0 < np.array([X, Y, Z], np.float32))).all(axis=1)
+            assert o["undef"][inside].mean() > 0.99 and inside.mean() > 0.5
+
+        cam, vp = rv.camera_from_pose((0.1 * X, 0.7 * Y, 0.1 * Z), -0.7, -np.pi - 0.3, W, H)
+        for flags in (rv.RV_FLAGS_REFERENCE, rv.RV_F_SHADOW):
+            r.frame(cam, vp, flags=flags)
+            ref = oracle.render(ow, oracle.make_frame(W, H, flags, rv.camera_dict(cam, vp)), want_stats=False)
+            assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref["rgba"]), flags
+            assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"]), flags
+            assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"]), flags
+            if flags & rv.RV_F_PREPASS:
+                assert np.array_equal(r.readback(rv.RV_IMAGE_HALF_DIST).view(np.uint32),
+                                      ref["halfdist"].view(np.uint32))
+    finally:
+        r.close()
+
+
+FLOW_WORLDS = [("pillars", (7, 7, 7)), ("sparse", (7, 7, 7)), ("full", (6, 6, 6)), ("blocks", (6, 5, 7))]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kind,dims", FLOW_WORLDS, ids=[w[0] for w in FLOW_WORLDS])
+def test_synthetic_world_drop_in_flow(rv, atlas, oracle, kind, dims):
+    """renderLoop's calls (UpdateGIData, drawCUDA with ref_compat, a moving camera) on the same
+    worlds: the one-launch flow frames equal drawCUDA's two launches image for image and GI grid
+    for grid, with no render wave falling back; the last frame and the grid equal the oracle."""
+    from rvgrt_amd.configs import camera_path
+    lx, ly, lz = dims
+    ow = oracle.OracleWorld(lx, ly, lz, atlas=atlas)
+    X, Y, Z = ow.X, ow.Y, ow.Z
+    vox = _voxels(kind, X, Y, Z, np.random.default_rng(sum(map(ord, kind))))
+    ow.bits[:] = np.packbits(vox.ravel(), bitorder="little").view(np.uint32)
+    ow.build_csdf()
+    ow.gi_init()
+    W, H, rays, nfr = 192, 128, 3000, 6
+    ngi = len(ow.gi) // 4
+    seq = camera_path(((0.1 * X, 0.7 * Y, 0.1 * Z), -0.7, -np.pi - 0.3), W, H, nfr, pan=0.03, ref_compat=True)
+    ctx = []
+    try:
+        for flow in (1, 0):
+            r = rv.StateRender(dims, W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas, gi_rays_per_frame=rays)
+            ctx.append(r)
+            r.world_import(rv.RV_WORLD_BITS, ow.bits)
+            r.csdf_build()
+            r.gi_init()
+            r.set_flow(flow)
+        a, b = ctx
+        for k in range(nfr):
+            for r in (a, b):
+                r.update_gi_data()
+                c = seq[k].cam
+                r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(seq[k].vp),
+                            np.ctypeslib.as_array(seq[k].prev_vp), 0.0, seq[k].time)
+            for kind_img in (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH, rv.RV_IMAGE_HALF_DIST,
+                             rv.RV_IMAGE_HALF_SHADOW):
+                assert np.array_equal(a.readback(kind_img), b.readback(kind_img)), (k, kind_img)
+        assert np.array_equal(a.world_export(rv.RV_WORLD_GI), b.world_export(rv.RV_WORLD_GI))
+        active, launches, fallbacks = a.flow_info()
+        assert active and launches == nfr and fallbacks == 0
+        off = 0
+        for fno in range(nfr):
+            ow.gi_update(fno, first=off, count=min(rays, ngi - off))
+            off = 0 if off + rays >= ngi else off + rays
+        assert np.array_equal(a.world_export(rv.RV_WORLD_GI), ow.gi)
+        d = seq[nfr - 1]
+        fr = oracle.make_frame(W, H, rv.RV_FLAGS_REFERENCE | rv.RV_F_REF_FETCH,
+                               rv.camera_dict(d.cam, np.ctypeslib.as_array(d.vp)), time=d.time,
+                               pvp=np.ctypeslib.as_array(d.prev_vp))
+        ref = oracle.render(ow, fr, want_stats=False)
+        assert np.array_equal(a.readback(rv.RV_IMAGE_COLOR), ref["rgba"])
+        assert np.array_equal(a.readback(rv.RV_IMAGE_MOTION), ref["mv"])
+        assert np.array_equal(a.readback(rv.RV_IMAGE_DEPTH), ref["depth"])
+    finally:
+        for r in ctx:
+            r.close()
