@@ -172,3 +172,51 @@ def test_synthetic_world_drop_in_flow(rv, atlas, oracle, kind, dims):
     finally:
         for r in ctx:
             r.close()
+
+
+def _basis(fo, up_hint):
+    fo = np.asarray(fo, np.float64)
+    fo /= np.linalg.norm(fo)
+    ri = np.cross(fo, up_hint)
+    ri /= np.linalg.norm(ri)
+    up = np.cross(fo, ri)
+    return [np.asarray(v, np.float32) for v in (fo, up, ri)]
+
+
+# (name, camera position, forward, up, right): exact axis-aligned bases put the centre column's rays on
+# zero direction components (the 1e10 deltaDist path) and integer positions on voxel faces
+CAMERAS = [
+    ("axis_z", (64.0, 40.0, 64.0), (0, 0, 1), (0, -1, 0), (1, 0, 0)),
+    ("down", (64.5, 120.0, 64.5), (0, -1, 0), (0, 0, 1), (1, 0, 0)),
+    ("axis_x_face", (0.0, 48.0, 64.0), (1, 0, 0), (0, -1, 0), (0, 0, -1)),
+    ("outside", (-40.0, 90.0, -40.0)) + tuple(_basis((1.0, -0.45, 1.0), (0, 1, 0))),
+    ("in_floor", (64.25, 5.0, 64.75)) + tuple(_basis((0.3, -0.2, 1.0), (0, 1, 0))),
+    ("corner", (0.0, 0.0, 0.0)) + tuple(_basis((1.0, 1.0, 1.0), (0, 1, 0))),
+]
+
+
+@pytest.mark.parametrize("name,pos,fo,up,ri", CAMERAS, ids=[c[0] for c in CAMERAS])
+def test_camera_edge_cases(rv, atlas, oracle, oracle_world, name, pos, fo, up, ri):
+    """Frames from cameras no pose of the bench takes -- looking exactly along an axis from an
+    integer position, straight down, from a voxel face at the grid's edge, from outside the grid,
+    from inside the solid floor (every primary ray the R2 undefined hit) and from the grid's
+    corner -- equal the oracle bit for bit (reference and C2 flags) on the procedural 128^3 world."""
+    ow = oracle_world(7, 7, 7, gi_sweeps=1)
+    W, H = 160, 96
+    r = rv.StateRender((7, 7, 7), W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+    try:
+        r.world_import(rv.RV_WORLD_BITS, ow.bits)
+        r.world_import(rv.RV_WORLD_CSDF, ow.csdf)
+        r.world_import(rv.RV_WORLD_GI, ow.gi)
+        _, vp = rv.camera_from_pose((12.8, 76.8, 12.8), -0.7, -np.pi - 0.3, W, H)
+        cam = rv._lib.rv_camera()
+        for k, v in (("pos", pos), ("forward", fo), ("up", up), ("right", ri)):
+            getattr(cam, k)[:] = [float(x) for x in np.asarray(v, np.float32)]
+        for flags in (rv.RV_FLAGS_REFERENCE, rv.RV_F_SHADOW):
+            r.frame(cam, vp, flags=flags)
+            ref = oracle.render(ow, oracle.make_frame(W, H, flags, rv.camera_dict(cam, vp)), want_stats=False)
+            assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref["rgba"]), flags
+            assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"]), flags
+            assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"]), flags
+    finally:
+        r.close()
