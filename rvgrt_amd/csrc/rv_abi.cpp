@@ -18,7 +18,7 @@ rv_status rv_create(const rv_config* cfg, int32_t device, rv_ctx** out) {
         return RV_ERR_INVALID;
     // brick records must stay below 4 GiB (32-bit gather offsets): <= 2^34 voxels
     if (cfg->log2_x + cfg->log2_y + cfg->log2_z > 34) return RV_ERR_INVALID;
-    if (cfg->width < 2 || cfg->height < 2 || (cfg->width & 1) || (cfg->height & 1)) return RV_ERR_INVALID;
+    if (cfg->width < 2 || cfg->height < 2) return RV_ERR_INVALID;   // any parity: half-res images floor(W/2) x floor(H/2)
     if (cfg->width > 32768 || cfg->height > 32768) return RV_ERR_INVALID;   // images < 4 GiB: 32-bit offsets
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return RV_ERR_NO_DEVICE;

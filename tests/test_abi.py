@@ -47,7 +47,9 @@ def test_invalid_config_rejected_without_touching_gpu():
     h = C.c_void_p()
     assert L.rv_create(C.byref(cfg), 0, C.byref(h)) == _lib.RV_ERR_INVALID
     cfg.log2_x = cfg.log2_y = cfg.log2_z = 6
-    cfg.width = 63                                  # odd width (half-res buffers need W/2)
+    cfg.width = 1                                   # no half-res image (floor(W / 2) = 0)
+    assert L.rv_create(C.byref(cfg), 0, C.byref(h)) == _lib.RV_ERR_INVALID
+    cfg.width, cfg.height = 64, 32769               # images past 32-bit offsets
     assert L.rv_create(C.byref(cfg), 0, C.byref(h)) == _lib.RV_ERR_INVALID
     assert L.rv_frame(None, None, None, None, 0.0, 0.0, 0.0, 0) == _lib.RV_ERR_INVALID
     assert L.rv_destroy(None) is None

@@ -220,3 +220,119 @@ def test_camera_edge_cases(rv, atlas, oracle, oracle_world, name, pos, fo, up, r
             assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"]), flags
     finally:
         r.close()
+
+
+ODD_SIZES = [(161, 97), (67, 33), (1000, 7), (2, 2), (130, 258), (1707, 961)]
+
+
+@pytest.mark.parametrize("W,H", ODD_SIZES)
+def test_odd_resolutions(rv, atlas, oracle, oracle_world, W, H):
+    """Frame sizes off every tile grid -- odd (a DLSS render size such as 1707 x 961 for a 2560 x
+    1441 window), tiny, one-texel-high half-res images, taller than wide: the two-launch frame and
+    the drop-in flow frame (renderLoop's calls) equal the oracle.  The half-res images are
+    floor(W / 2) x floor(H / 2) as the reference's (src/StateRender.cu:150-151,318-325)."""
+    from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    ow = oracle_world(7, 7, 7, gi_sweeps=1)
+    seq = camera_path(TEST_POSES_128["P0"], W, H, 2, pan=0.01, ref_compat=True)
+    d = seq[1]
+    for flow in (0, 1):
+        r = rv.StateRender((7, 7, 7), W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+        try:
+            r.world_import(rv.RV_WORLD_BITS, ow.bits)
+            r.world_import(rv.RV_WORLD_CSDF, ow.csdf)
+            r.world_import(rv.RV_WORLD_GI, ow.gi)
+            r.set_flow(flow)
+            c = d.cam
+            r.draw_cuda(c.pos[:], c.forward[:], c.up[:], c.right[:], np.ctypeslib.as_array(d.vp),
+                        np.ctypeslib.as_array(d.prev_vp), 0.0, d.time)
+            fr = oracle.make_frame(W, H, rv.RV_FLAGS_REFERENCE | rv.RV_F_REF_FETCH,
+                                   rv.camera_dict(c, np.ctypeslib.as_array(d.vp)), time=d.time,
+                                   pvp=np.ctypeslib.as_array(d.prev_vp))
+            ref = oracle.render(ow, fr, want_stats=False)
+            assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref["rgba"]), flow
+            assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"]), flow
+            assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"]), flow
+        finally:
+            r.close()
+
+
+@pytest.mark.parametrize("W,H", ODD_SIZES)
+def test_odd_resolutions_wavefront_and_tiles(rv, atlas, oracle_world, W, H):
+    """The same sizes through the wavefront stages and through screen tiles (three "ranks" of
+    interleaved 16-px tiles with their own half-res halos, scattered back by rv_untile): both equal
+    the per-pixel frame."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    ow = oracle_world(7, 7, 7, gi_sweeps=1)
+    cam, vp = rv.camera_from_pose(*TEST_POSES_128["P1"], W, H)
+
+    def ctx():
+        r = rv.StateRender((7, 7, 7), W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+        r.world_import(rv.RV_WORLD_BITS, ow.bits)
+        r.world_import(rv.RV_WORLD_CSDF, ow.csdf)
+        r.world_import(rv.RV_WORLD_GI, ow.gi)
+        return r
+
+    full = ctx()
+    wf = ctx()
+    sink = ctx()
+    try:
+        full.frame(cam, vp)
+        want = [full.readback(k).copy() for k in (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH)]
+        wf.set_frame_path("wavefront")
+        wf.frame(cam, vp)
+        for k, img in zip((rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH), want):
+            assert np.array_equal(wf.readback(k), img), k
+        T = 16
+        ids_all = np.arange(((W + T - 1) // T) * ((H + T - 1) // T), dtype=np.int32)
+        for rank in range(3):
+            ids = ids_all[rank::3]
+            if not len(ids):
+                continue
+            rr = ctx()
+            try:
+                rr.frame_tiles(cam, vp, ids, tile_px=T)
+                rr.sync()
+                p, nbytes = rr.tile_buffer()
+                assert nbytes >= len(ids) * T * T * 4
+                sink.untile(p, ids, tile_px=T)
+                sink.sync()
+            finally:
+                rr.close()
+        assert np.array_equal(sink.readback(rv.RV_IMAGE_COLOR), want[0])
+    finally:
+        for r in (full, wf, sink):
+            r.close()
+
+
+@pytest.mark.parametrize("W,H", [(161, 97), (1707, 961)])
+@pytest.mark.parametrize("loop", ["pipelined", "grouped"])
+def test_odd_resolutions_frame_loops(rv, atlas, W, H, loop):
+    """The native loops at odd sizes: rv_render_frame_seq pipelined (k_ref_pipe) and in groups of 4
+    (k_ref_group) on a moving camera equal UpdateGIData + one frame at a time, images and GI grid."""
+    from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    flags, rays = rv.RV_FLAGS_REFERENCE, 3000
+    seq = camera_path(TEST_POSES_128["P0"], W, H, 7, pan=0.01, ref_compat=True)
+
+    def make():
+        r = rv.StateRender((7, 7, 7), W, H, flags=flags, atlas=atlas, gi_rays_per_frame=rays)
+        r.world_build()
+        r.gi_update(0)
+        return r
+
+    ref, r = make(), make()
+    try:
+        ref.set_pipeline(0)
+        if loop == "grouped":
+            r.set_frame_group(4)
+        for a, b in ((0, 3), (3, 6)):
+            r.render_frame_seq(seq[a:b], next_desc=seq[b], flags=flags, gi_per_frame=True)
+            for d in seq[a:b]:
+                ref.update_gi_data()
+                ref.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time,
+                          jx=d.jitter_x, jy=d.jitter_y, flags=flags)
+            for k in (rv.RV_IMAGE_COLOR, rv.RV_IMAGE_MOTION, rv.RV_IMAGE_DEPTH, rv.RV_IMAGE_HALF_DIST):
+                assert np.array_equal(r.readback(k), ref.readback(k)), (a, k)
+            assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ref.world_export(rv.RV_WORLD_GI)), a
+    finally:
+        r.close()
+        ref.close()
