@@ -336,3 +336,69 @@ def test_odd_resolutions_frame_loops(rv, atlas, W, H, loop):
     finally:
         r.close()
         ref.close()
+
+
+@pytest.mark.parametrize("flags,T,N,grp", [(8, 16, 3, 0), (7, 16, 3, 0), (7, 32, 2, 3)])
+def test_odd_resolution_loopback_ranks(rv, atlas, flags, T, N, grp):
+    """The N-rank loop (loopback communicator, one host thread per rank; see test_gpu_multirank.py) at
+    161 x 97: partial tiles on the right and bottom edges, the gather and rank 0's assembly -- rank 0's
+    frames and every rank's GI grid equal one context rendering whole frames one at a time."""
+    import threading
+    from rvgrt_amd.configs import TEST_POSES_128, camera_path
+    W, H, rays = 161, 97, 3000
+    gi = bool(flags & rv.RV_F_GI)
+    seq = camera_path(TEST_POSES_128["P0"], W, H, 7, pan=0.02, ref_compat=True)
+
+    def make():
+        r = rv.StateRender((7, 7, 7), W, H, flags=flags, atlas=atlas, gi_rays_per_frame=rays)
+        r.world_build()
+        r.gi_update(0)
+        return r
+
+    ref = make()
+    ref.set_pipeline(0)
+    group = rv.LoopbackGroup(N, timeout_ms=60000)
+    rs = [make() for _ in range(N)]
+    comms = []
+    try:
+        for q, r in enumerate(rs):
+            if not gi:
+                r.set_frames_in_flight(4)
+            r.set_tile_shard(T, q, N)
+            r.set_frame_group(grp)
+            comms.append(rv.Comm.loopback(r, group, q))
+        errs = [None] * N
+
+        def body(q):
+            try:
+                rs[q].render_frame_seq(seq[0:6], next_desc=seq[6], flags=flags, gi_per_frame=gi, comm=comms[q])
+            except BaseException as e:   # noqa: BLE001 -- re-raised below
+                errs[q] = e
+        ts = [threading.Thread(target=body, args=(q,)) for q in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=300)
+            assert not t.is_alive(), "a rank thread hung"
+        for e in errs:
+            if e is not None:
+                raise e
+        for c in comms:
+            c.wait(60000)
+        for d in seq[0:6]:
+            if gi:
+                ref.update_gi_data()
+            ref.frame(d.cam, np.ctypeslib.as_array(d.vp), np.ctypeslib.as_array(d.prev_vp), time=d.time,
+                      jx=d.jitter_x, jy=d.jitter_y, flags=flags)
+        assert np.array_equal(rs[0].readback(rv.RV_IMAGE_COLOR), ref.readback(rv.RV_IMAGE_COLOR))
+        if gi:
+            want = ref.world_export(rv.RV_WORLD_GI)
+            for q, r in enumerate(rs):
+                assert np.array_equal(r.world_export(rv.RV_WORLD_GI), want), q
+    finally:
+        for c in comms:
+            c.close()
+        for r in rs:
+            r.close()
+        group.close()
+        ref.close()
