@@ -59,3 +59,21 @@ def test_under_torch_distributed_run():
     assert p.returncode == 0, p.stderr[-2000:]
     recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(recs) == 1 and recs[0]["n_gpus"] == 2
+
+
+def test_resolution_override():
+    """--resolution keeps the config's world, flags and GI schedule and changes only the frame size
+    (odd sizes included); the metric's description names the new size."""
+    import importlib
+    import sys as _sys
+    _sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    from rvgrt_amd.configs import CONFIGS
+    c = bench.bench_config("c4", "1707x961")
+    base = CONFIGS["c4"]
+    assert (c.width, c.height) == (1707, 961)
+    assert (c.log2_n, c.flags, c.gi_sweeps, c.gi_per_frame) == (base.log2_n, base.flags, base.gi_sweeps, base.gi_per_frame)
+    assert "1707x961" in c.describe and "3840x2160" not in c.describe
+    assert bench.bench_config("c3") is CONFIGS["c3"]
+    with pytest.raises(SystemExit):
+        bench.bench_config("c3", "1x5")
