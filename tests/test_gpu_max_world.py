@@ -12,7 +12,6 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-DIMS = (12, 10, 12)
 
 
 @pytest.fixture(scope="module")
@@ -23,10 +22,11 @@ def rv():
 
 
 @pytest.mark.timeout(900)
-def test_max_world_build_and_frame(rv, atlas, oracle):
-    lx, ly, lz = DIMS
+@pytest.mark.parametrize("dims", [(12, 10, 12), (13, 8, 13)], ids=["4096x1024x4096", "8192x256x8192"])
+def test_max_world_build_and_frame(rv, atlas, oracle, dims):
+    lx, ly, lz = dims
     W, H = 1920, 1080
-    r = rv.StateRender(DIMS, W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+    r = rv.StateRender(dims, W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
     try:
         r.world_build()
         bits = r.world_export(rv.RV_WORLD_BITS)
@@ -62,7 +62,7 @@ def test_max_world_build_and_frame(rv, atlas, oracle):
         del gi
 
         # a reference frame: rows against the oracle on the same world
-        pos = (0.1 * X, 350.0, 0.1 * Z)
+        pos = (0.1 * X, min(350.0, 0.9 * Y), 0.1 * Z)
         cam, vp = rv.camera_from_pose(pos, -0.7, -np.pi - 0.3, W, H)
         r.frame(cam, vp, flags=rv.RV_FLAGS_REFERENCE)
         img = r.readback(rv.RV_IMAGE_COLOR)
@@ -71,5 +71,32 @@ def test_max_world_build_and_frame(rv, atlas, oracle):
                                  want_stats=False)
         assert np.array_equal(img[rows], ref["rgba"][rows])
         assert len(np.unique(img[rows].reshape(-1, 4), axis=0)) > 50       # terrain, water and sky
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("dims", [(4, 4, 4), (4, 11, 4), (9, 4, 5)], ids=["16^3", "16x2048x16", "512x16x32"])
+def test_smallest_and_thinnest_worlds(rv, atlas, oracle, dims):
+    """The smallest world (16^3: two bricks a side, GI grid 4^3) and one-brick-thin ones: the whole
+    world (bits, CSDF, GI init and a sweep) and whole reference frames equal the oracle's own build."""
+    lx, ly, lz = dims
+    W, H = 96, 64
+    ow = oracle.OracleWorld(lx, ly, lz, atlas=atlas).build(gi_sweeps=1)
+    r = rv.StateRender(dims, W, H, flags=rv.RV_FLAGS_REFERENCE, atlas=atlas)
+    try:
+        r.world_build()
+        r.gi_update(0)
+        assert np.array_equal(r.world_export(rv.RV_WORLD_BITS), ow.bits)
+        assert np.array_equal(r.world_export(rv.RV_WORLD_CSDF), ow.csdf)
+        assert np.array_equal(r.world_export(rv.RV_WORLD_GI), ow.gi)
+        X, Y, Z = ow.X, ow.Y, ow.Z
+        for pos in ((0.5 * X, min(0.9 * Y, 60.0), 0.5 * Z), (-3.0, 0.5 * Y, -3.0)):
+            cam, vp = rv.camera_from_pose(pos, -0.7, -np.pi - 0.3, W, H)
+            r.frame(cam, vp, flags=rv.RV_FLAGS_REFERENCE)
+            ref = oracle.render(ow, oracle.make_frame(W, H, rv.RV_FLAGS_REFERENCE, rv.camera_dict(cam, vp)),
+                                want_stats=False)
+            assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref["rgba"]), pos
+            assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"]), pos
+            assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"]), pos
     finally:
         r.close()
