@@ -402,3 +402,28 @@ def test_odd_resolution_loopback_ranks(rv, atlas, flags, T, N, grp):
             r.close()
         group.close()
         ref.close()
+
+
+@pytest.mark.parametrize("flags", list(range(16)) + [33, 39, 41])
+def test_every_feature_combination(rv, atlas, oracle, oracle_world, flags):
+    """Every combination of the frame's feature bits (pre-pass 1, water 2, GI 4, full-res shadow 8;
+    plus the reference texel fetch 32 where a pre-pass exists), not only the bench's sets: the library's
+    dispatch (compiled feature sets or the dynamic-feature kernel) equals the oracle on both poses."""
+    from rvgrt_amd.configs import TEST_POSES_128
+    ow = oracle_world(7, 7, 7, gi_sweeps=1)
+    W, H = 160, 96
+    r = rv.StateRender((7, 7, 7), W, H, flags=flags, atlas=atlas)
+    try:
+        r.world_import(rv.RV_WORLD_BITS, ow.bits)
+        r.world_import(rv.RV_WORLD_CSDF, ow.csdf)
+        r.world_import(rv.RV_WORLD_GI, ow.gi)
+        for pose in ("P0", "P1"):
+            cam, vp = rv.camera_from_pose(*TEST_POSES_128[pose], W, H)
+            r.frame(cam, vp, flags=flags, time=0.25)
+            ref = oracle.render(ow, oracle.make_frame(W, H, flags, rv.camera_dict(cam, vp), time=0.25),
+                                want_stats=False)
+            assert np.array_equal(r.readback(rv.RV_IMAGE_COLOR), ref["rgba"]), pose
+            assert np.array_equal(r.readback(rv.RV_IMAGE_MOTION), ref["mv"]), pose
+            assert np.array_equal(r.readback(rv.RV_IMAGE_DEPTH), ref["depth"]), pose
+    finally:
+        r.close()
