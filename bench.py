@@ -114,19 +114,26 @@ def binding_limit(tj: dict, launch_ms: float):
             "hbm_traffic": round(hbm, 3), "source": os.path.relpath(tj.get("_path", ""), ROOT) if tj.get("_path") else None}
 
 
-def bench_config(name, resolution=None):
-    """CONFIGS[name], or its world and frame at another frame size ("WxH", any >= 2, odd too)."""
+def bench_config(name, resolution=None, world=None):
+    """CONFIGS[name], or its frame at another size ("WxH", any >= 2, odd too) and / or on a cubic world
+    of another size (`world` = log2 of the side, 4..11)."""
     import dataclasses
     import re
     from rvgrt_amd.configs import CONFIGS
     cfg = CONFIGS[name]
-    if not resolution:
-        return cfg
-    rw, rh = (int(v) for v in resolution.lower().split("x"))
-    if rw < 2 or rh < 2:
-        raise SystemExit(f"--resolution {resolution}: each side must be >= 2")
-    return dataclasses.replace(cfg, width=rw, height=rh,
-                               describe=re.sub(r"\d+x\d+", f"{rw}x{rh}", cfg.describe, count=1))
+    if resolution:
+        rw, rh = (int(v) for v in resolution.lower().split("x"))
+        if rw < 2 or rh < 2:
+            raise SystemExit(f"--resolution {resolution}: each side must be >= 2")
+        cfg = dataclasses.replace(cfg, width=rw, height=rh,
+                                  describe=re.sub(r"\d+x\d+", f"{rw}x{rh}", cfg.describe, count=1))
+    if world:
+        if not 4 <= int(world) <= 11:
+            raise SystemExit(f"--world {world}: log2 of the cube side, 4 .. 11")
+        n = 1 << int(world)
+        cfg = dataclasses.replace(cfg, log2_n=int(world),
+                                  describe=re.sub(r"\d+\^3", f"{n}^3", cfg.describe, count=1))
+    return cfg
 
 
 def main():
@@ -144,6 +151,8 @@ def main():
                     help="c1..c5 (default c4: 1024^3, 3840x2160, the reference frame with 2-bounce GI and a GI "
                          "update every frame -- the north star's 1-GPU workload, BASELINE configs[3])")
     ap.add_argument("--pose", default="P0")
+    ap.add_argument("--world", type=int, default=None,
+                    help="log2 of a cubic world's side (4..11): the config's frame on another world size")
     ap.add_argument("--resolution", default=None,
                     help="WxH: the config's world and frame at another frame size (e.g. 1707x961, a DLSS render size)")
     ap.add_argument("--camera", default="path", choices=["path", "static"],
@@ -252,7 +261,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    cfg = bench_config(args.config, args.resolution)
+    cfg = bench_config(args.config, args.resolution, args.world)
     gi_per_frame = cfg.gi_per_frame if args.gi_per_frame is None else bool(args.gi_per_frame)
     W, H = cfg.width, cfg.height
     flags = cfg.flags if args.flags is None else args.flags

@@ -77,3 +77,16 @@ def test_resolution_override():
     assert bench.bench_config("c3") is CONFIGS["c3"]
     with pytest.raises(SystemExit):
         bench.bench_config("c3", "1x5")
+
+
+def test_world_override():
+    import importlib
+    import sys as _sys
+    _sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    c = bench.bench_config("c4", world=9)
+    assert c.log2_n == 9 and c.n == 512 and "512^3" in c.describe and "1024^3" not in c.describe
+    c = bench.bench_config("c4", "1280x720", 11)
+    assert (c.width, c.height, c.n) == (1280, 720, 2048)
+    with pytest.raises(SystemExit):
+        bench.bench_config("c4", world=12)
