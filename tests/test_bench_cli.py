@@ -90,3 +90,28 @@ def test_world_override():
     assert (c.width, c.height, c.n) == (1280, 720, 2048)
     with pytest.raises(SystemExit):
         bench.bench_config("c4", world=12)
+
+
+def test_recorded_bench_line_keeps_the_contract():
+    """The bench line the driver parses, as last recorded on the GPU (profiles/r06/final/driver_bench.json):
+    every contract key, the roofline object (algorithmic bytes / launch time against the 8 TB/s peak,
+    with the PMC traffic) and the CPU baseline object."""
+    path = os.path.join(ROOT, "profiles", "r06", "final", "driver_bench.json")
+    d = json.loads(open(path).read().strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["vs_baseline"] is None
+    assert d["config"]["workload"] == "c4" and "model" not in d["config"]
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # achieved = algorithmic bytes per launch / the measured launch time
+    assert abs(rf["achieved"] - rf["algorithmic_bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9) < 0.01 * rf["achieved"]
+    assert rf["traffic"] and rf["traffic"] > 0
+    cb = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cb, k
+    assert cb["kind"] == "port" and cb["cores"] >= 1
+    # value = rays per frame x frames per second
+    assert abs(d["value"] - d["rays_per_frame"] / (d["ms_per_step"] * 1e-3) / 1e6) < 0.01 * d["value"]
