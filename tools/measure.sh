@@ -22,6 +22,9 @@
 #   tools/measure.sh tile-alone CFG POSE FRAMES    flow-launch timelines (tools/flow_waves.py, the diag build in
 #                                                  rvgrt_amd/variants/diag): whole, pre-pass alone, the longest
 #                                                  pre-pass tile alone                  -> gpurun_out/<TAG>_fw_*.log
+#   tools/measure.sh flow-ablation [CFG POSE N]     the drop-in k_ref_flow itemised: full, no GI window, pre-pass +
+#                                                  GI, pre-pass alone, the longest pre-pass tile alone (diag build)
+#   tools/measure.sh tile-warm [CFG POSE]          the longest pre-pass tile alone, cold vs its lines left in L2
 # TAG (env, default r05) prefixes every output; STEPS/WARMUP (env) size the bench runs (default 200/20).
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
